@@ -1,0 +1,1662 @@
+// scpqp.hip — MI355X (gfx950) batched SCP-QP trajectory planner.
+//
+// One workgroup (256 threads = 4 wave64) owns one problem at a time — one
+// joint multi-vehicle QCQP of one MPC step — and runs the whole hot path of
+// the reference for it without leaving the device:
+//
+//   K2  reference sampling            SampleReferTraj.py:8-122, MPC_Iter.py:35-43
+//   K1  Jacobian + expm + prediction  Model.py:45-87, MPC_Iter.py:59-149
+//   K3  constraint linearisation      SCP_controller.py:93-128 (factored, A.5)
+//   K4  convexified QP                SCP_controller.py:118-150 (IPM + polish)
+//   K3' QCQP evaluation               SCP_controller.py:215-265
+//   K5  SCP loop + stopping rule      SCP_controller.py:40-49,74-197
+//
+// Problems are pulled from a device work counter, so workgroups that finish
+// early (fewer SCP iterations, shorter horizon) immediately take the next one.
+// Everything is fp64.  The per-problem state (KKT matrix, Toeplitz blocks,
+// interior-point vectors) lives in LDS; when it does not fit (8 vehicles at
+// Hp=30), the KKT matrix and/or the constraint vectors move to a per-workgroup
+// global workspace (template flags H_G / V_G).
+//
+// The QP is solved in scaled variables (controls in units of
+// uLim, every constraint row of unit norm) by a Mehrotra predictor-corrector
+// interior point method on the normal equations
+//     K = P + G' D G,   P = blkdiag(2 Phi0, 0),
+// assembled from the Toeplitz structure:  K_uu = B'(2Q + W)B + diag,  with B
+// the block-Toeplitz prediction matrix (g_m = C A^m B) and W block-diagonal
+// per prediction step (2nVeh x 2nVeh blocks) — never the dense
+// (nVeh-1) x nVeh x Hp x N x N tensors of QCQP_formulate.  The IPM is followed
+// by an active-set polish (proximal method of multipliers on the identified
+// active set, same assembly / Cholesky / triangular solves) that returns the
+// exact minimiser when it certifies.
+
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <new>
+
+#include "scpqp.h"
+
+#define NT 256
+#define NWAVE (NT / 64)
+#define SCR_PER_WAVE 640
+
+namespace {
+
+// ---------------------------------------------------------------------------
+// Parameters (device copy of scpqp_params with derived constants)
+// ---------------------------------------------------------------------------
+struct DevParams {
+    int nV, hpMax, nO, maxPts;
+    int maxScp, maxIpm, nRefine, flags;
+    double dt, uLim, ctol, deltaTol, slackW, ipmTol, polDelta, polRho;
+    double Lf[SCPQP_MAX_VEH], Lr[SCPQP_MAX_VEH], Q[SCPQP_MAX_VEH], Qf[SCPQP_MAX_VEH],
+        R[SCPQP_MAX_VEH];
+    double D2veh[SCPQP_MAX_VEH * SCPQP_MAX_VEH];   // (dsafe + dsafeExtra)^2
+    double D2obs[SCPQP_MAX_VEH * SCPQP_MAX_OBST];
+    double poly[SCPQP_MAX_VEH * SCPQP_MAX_REFPTS * 2];
+    int npts[SCPQP_MAX_VEH];
+};
+
+enum Mode { MODE_SOLVE = 0, MODE_LINEARIZE = 1, MODE_EVALUATE = 2, MODE_SAMPLE = 3 };
+
+struct KArgs {
+    const DevParams* P;
+    int B, mode, maxScp, pad0;
+    const double *x0, *u0, *ec, *obst, *refIn, *uWarm, *uEval;
+    const int* hp;
+    double *uOut, *trajOut, *obj, *maxv, *sumv;
+    int *status, *nscp, *nipm, *feas;
+    double *Ad, *Bd, *Ed, *gOut, *p0Out, *psiOut, *refOut;
+    double *cveh, *cobs;
+    double* ws;
+    long long wsStride;
+    int* counter;
+};
+
+// ---------------------------------------------------------------------------
+// Per-problem layout.  Sizes allocate for hp_max; indexing uses the problem's
+// own horizon Hb, so a mixed-horizon batch shares one launch.
+// ---------------------------------------------------------------------------
+struct Lay {
+    int V, O, Hb, N, n, m, mc, ld, mp, nb;
+    double *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
+    double *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr;
+    int* rinfo;
+    double *H, *Wt;
+    double *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
+};
+
+__host__ __device__ inline int pad2(int x) { return (x + 1) & ~1; }
+
+struct Sizes {
+    int persist, uni, ws;   // doubles
+};
+
+// Carve the layout; with null bases only sizes are computed (host planning).
+__host__ __device__ inline Sizes carve(Lay* L, double* lds, double* ws, int V, int O, int Hm,
+                                       int Hb, bool hG, bool vG) {
+    const int N = V * Hm, n = N + 1, m = V * (V - 1) / 2 * Hm + V * O * Hm;
+    const int mc = m + 2 * N + 1, ld = n | 1, nb = V * (V + 1) / 2;
+    int p = 0;
+    auto take = [&](double** dst, int cnt) {
+        if (lds && dst) *dst = lds + p;
+        p += pad2(cnt);
+    };
+    take(L ? &L->x0 : nullptr, 6 * V);
+    take(L ? &L->u0 : nullptr, V);
+    take(L ? &L->ec : nullptr, 2 * V);
+    take(L ? &L->g : nullptr, 2 * V * Hm);
+    take(L ? &L->p0 : nullptr, 2 * V * Hm);
+    take(L ? &L->ref : nullptr, 2 * V * Hm);
+    take(L ? &L->ob : nullptr, 2 * O * Hm);
+    take(L ? &L->ub : nullptr, V * Hm);
+    take(L ? &L->pb : nullptr, 2 * V * Hm);
+    take(L ? &L->ya : nullptr, 2 * V * Hm);
+    take(L ? &L->yb : nullptr, 2 * V * Hm);
+    take(L ? &L->qs : nullptr, V * Hm);
+    take(L ? &L->rowE : nullptr, 2 * m);
+    take(L ? &L->rowW : nullptr, m);
+    take(L ? &L->rowH : nullptr, m);
+    {
+        double* ri = nullptr;
+        take(&ri, (m + 1) / 2);
+        if (L && lds) L->rinfo = reinterpret_cast<int*>(ri);
+    }
+    take(L ? &L->z : nullptr, n);
+    take(L ? &L->dz : nullptr, n);
+    take(L ? &L->rhs : nullptr, n);
+    take(L ? &L->rd : nullptr, n);
+    take(L ? &L->dinv : nullptr, n);
+    take(L ? &L->red : nullptr, 64);
+    Sizes S;
+    S.persist = p;
+    // union region: setup scratch  |  solve arrays
+    const int setup = NWAVE * SCR_PER_WAVE;
+    int u = 0, w = 0;
+    auto takeU = [&](double** dst, int cnt, bool global) {
+        if (global) {
+            if (ws && dst) *dst = ws + w;
+            w += pad2(cnt);
+        } else {
+            if (lds && dst) *dst = lds + p + u;
+            u += pad2(cnt);
+        }
+    };
+    takeU(L ? &L->H : nullptr, n * ld, hG);
+    takeU(L ? &L->Wt : nullptr, 4 * Hm * nb, false);
+    double** vec[9] = {nullptr};
+    if (L) {
+        vec[0] = &L->s; vec[1] = &L->lam; vec[2] = &L->ds; vec[3] = &L->dl; vec[4] = &L->rp;
+        vec[5] = &L->dd; vec[6] = &L->sa; vec[7] = &L->la; vec[8] = &L->tv;
+    }
+    for (int i = 0; i < 9; ++i) takeU(vec[i], mc, vG);
+    if (L && lds) L->scr = lds + p;
+    S.uni = u > setup ? u : setup;
+    S.ws = w;
+    if (L) {
+        L->V = V; L->O = O; L->Hb = Hb; L->N = V * Hb; L->n = L->N + 1;
+        L->mp = V * (V - 1) / 2 * Hb;
+        L->m = L->mp + V * O * Hb;
+        L->mc = L->m + 2 * L->N + 1;
+        L->ld = ld;           // allocation leading dimension (odd: conflict-free columns)
+        L->nb = nb;
+    }
+    return S;
+}
+
+// ---------------------------------------------------------------------------
+// Small helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    long long bits = __double_as_longlong(v);
+    int lo = __builtin_amdgcn_readlane(static_cast<int>(bits & 0xffffffffll), lane);
+    int hi = __builtin_amdgcn_readlane(static_cast<int>(bits >> 32), lane);
+    return __longlong_as_double((static_cast<long long>(hi) << 32) |
+                                (static_cast<unsigned int>(lo)));
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+// Reduce four values across the workgroup; ops: bit q set = max, else sum.
+// (min is expressed as max of negated values by callers.)
+__device__ __forceinline__ void block_reduce4(double* v, int maxmask, double* red) {
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (maxmask >> q & 1) ? wave_max(v[q]) : wave_sum(v[q]);
+    __syncthreads();
+    if (l == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) red[w * 4 + q] = v[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        double r = red[q];
+#pragma unroll
+        for (int ww = 1; ww < NWAVE; ++ww)
+            r = (maxmask >> q & 1) ? fmax(r, red[ww * 4 + q]) : r + red[ww * 4 + q];
+        v[q] = r;
+    }
+}
+
+__device__ __forceinline__ int pair_index(int i, int j, int V) {
+    return i * (2 * V - i - 1) / 2 + (j - i - 1);
+}
+
+// Row r -> (i, j, o, k): vehicle pair rows (i<j, k innermost) then obstacle
+// rows (v, o, k) — the order of SCP_controller.py:97-114.
+__device__ __forceinline__ void row_decode(const Lay& L, int info, int& i, int& j, int& o,
+                                           int& k) {
+    i = info & 0xff;
+    j = ((info >> 8) & 0xff) - 1;
+    o = ((info >> 16) & 0xff) - 1;
+    k = (info >> 24) & 0xff;
+}
+
+__device__ __forceinline__ double hval(const Lay& L, int i) {
+    return i < L.m ? L.rowH[i] : (i < L.mc - 1 ? 1.0 : 0.0);
+}
+
+// ---------------------------------------------------------------------------
+// Vehicle model (Model.py:45-87)
+// ---------------------------------------------------------------------------
+__device__ void bicycle_jacobian(const double* x, double u, double Lf, double Lr, double n0,
+                                 double n1, double Ac[6][6], double Ec[6]) {
+    const double L = Lf + Lr, rho = Lr / L;
+    const double v = x[3], psi = x[2], d = x[5];
+    const double t = tan(d), sec2 = t * t + 1.0;
+    const double kap = sqrt(rho * rho * t * t + 1.0);
+    const double beta = atan(rho * t);
+    const double th = psi + beta;
+    const double cth = cos(th), sth = sin(th);
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+        for (int j = 0; j < 6; ++j) Ac[i][j] = 0.0;
+    Ac[0][2] = -v * sth * kap;
+    Ac[0][3] = cth * kap;
+    Ac[0][5] = rho * rho * v * cth * t * sec2 / kap - rho * v * sth * sec2 / kap;
+    Ac[1][2] = v * cth * kap;
+    Ac[1][3] = sth * kap;
+    Ac[1][5] = rho * v * cth * sec2 / kap + rho * rho * v * sth * t * sec2 / kap;
+    Ac[2][3] = t / L;
+    Ac[2][5] = v * sec2 / L;
+    Ac[3][4] = 1.0;
+    Ac[5][5] = -10.0;
+    // f(x, u) (Model.py:69-87) with the two noise draws on dx[0], dx[1]
+    const double vc = v * sqrt(1.0 + (rho * t) * (rho * t));
+    double f[6];
+    f[0] = vc * cos(psi + beta) + n0;
+    f[1] = vc * sin(psi + beta) + n1;
+    f[2] = vc * t * cos(beta) / L;
+    f[3] = x[4];
+    f[4] = 0.0;
+    f[5] = (u - x[5]) / 0.1;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+        double ax = 0.0;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) ax += Ac[i][j] * x[j];
+        Ec[i] = f[i] - ax - (i == 5 ? 10.0 * u : 0.0);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Reference sampler (SampleReferTraj.py:8-122), one lane per vehicle.
+// Quirks B.1 (alternation past the end) and B.3 (rear-axle speed) reproduced;
+// B.2's float '^' (reference raises) is evaluated with '**' and flagged.
+// ---------------------------------------------------------------------------
+__device__ int sample_reference(const DevParams& P, int v, double vx, double vy, double step,
+                                int Hb, double* out /* [Hb][2] */) {
+    const double* c = P.poly + v * P.maxPts * 2;
+    const int np = P.npts[v];
+    int flag = 0;
+    // getShortestDistance: seeded with curve point 1, index 2 (quirk B.2)
+    double xm = c[2], ym = c[3];
+    double dmin = sqrt((vx - c[2]) * (vx - c[2]) + (vy - c[3]) * (vy - c[3]));
+    int imin = 2;
+    for (int j = 1; j < np; ++j) {
+        const double x1 = c[2 * (j - 1)], y1 = c[2 * (j - 1) + 1], x2 = c[2 * j], y2 = c[2 * j + 1];
+        const double bl = sqrt((x2 - x1) * (x2 - x1) + (y2 - y1) * (y2 - y1));
+        double xp, yp, sd, lam;
+        if (bl != 0.0) {
+            const double xn = (x2 - x1) / bl, yn = (y2 - y1) / bl;
+            const double x31 = vx - x1, y31 = vy - y1;
+            const double dot = xn * x31 + yn * y31;
+            sd = xn * y31 - yn * x31;
+            xp = x1 + dot * xn;
+            yp = y1 + dot * yn;
+            lam = dot / bl;
+        } else {
+            sd = sqrt((vx - x1) * (vx - x1) + (vy - y1) * (vy - y1));
+            lam = 0.0;
+            xp = x1;
+            yp = y1;
+        }
+        if ((0.0 < lam || j == 1) && (lam < 1.0 || j == np - 1)) {
+            if (fabs(sd) < fabs(dmin)) {
+                xm = xp; ym = yp; dmin = sd; imin = j;
+            }
+        } else {
+            flag = 1;   // reference raises TypeError here (float ^ int)
+            const double de = sqrt((vx - x2) * (vx - x2) + (vy - y2) * (vy - y2));
+            if (de < fabs(dmin)) {
+                xm = x2; ym = y2; dmin = (sd > 0.0) ? de : ((sd < 0.0) ? -de : 0.0); imin = j;
+            }
+        }
+    }
+    for (int i = 0; i + 1 < np; ++i) {
+        const double dx = c[2 * i + 2] - c[2 * i], dy = c[2 * i + 3] - c[2 * i + 1];
+        if (!(sqrt(dx * dx + dy * dy) > step)) flag = 1;   // SampleReferTraj.py:18-19 assert
+    }
+    int idx = imin;
+    if (idx > np - 1) {   // vehicle exactly on the endpoint: reference raises IndexError
+        idx = np - 1;
+        flag = 1;
+    }
+    double cx = xm, cy = ym;
+    for (int i = 0; i < Hb; ++i) {
+        const double ex = c[2 * idx], ey = c[2 * idx + 1];
+        const double rem = sqrt((cx - ex) * (cx - ex) + (cy - ey) * (cy - ey));
+        if (rem > step || idx == np) {
+            const double dx = ex - c[2 * idx - 2], dy = ey - c[2 * idx - 1];
+            const double nr = sqrt(dx * dx + dy * dy);
+            cx = cx + step * (dx / nr);
+            cy = cy + step * (dy / nr);
+        } else {
+            cx = ex; cy = ey;
+            idx = idx < np - 1 ? idx : np - 1;
+            const double dx = c[2 * idx] - c[2 * idx - 2], dy = c[2 * idx + 1] - c[2 * idx - 1];
+            const double nr = sqrt(dx * dx + dy * dy);
+            cx = cx + (step - rem) * (dx / nr);
+            cy = cy + (step - rem) * (dy / nr);
+        }
+        out[2 * i] = cx;
+        out[2 * i + 1] = cy;
+    }
+    return flag;
+}
+
+// ---------------------------------------------------------------------------
+// 8x8 matrix exponential, one wave per vehicle, lane = entry (i = lane>>3,
+// j = lane&7).  Pade-13 with scaling and squaring (Higham 2005; the algorithm
+// family of scipy.linalg.expm used at MPC_Iter.py:106,111).  The single 8x8
+// expm(dt [[Ac Bc Ec];0]) gives Ad, Bd and Ed at once.
+// All waves execute the same barrier sequence (`act` masks the work).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double mm_entry(const double* A, const double* B, int i, int j) {
+    double acc = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc += A[i * 8 + k] * B[k * 8 + j];
+    return acc;
+}
+
+__device__ void expm8(double* scr, bool act, double* red) {
+    // scr: M(0) A(64) A2(128) A4(192) A6(256) T1(320) T2(384) U(448) Vv(512) aug(0..127 reuse M,A)
+    const int lane = threadIdx.x & 63, i = lane >> 3, j = lane & 7;
+    double* M = scr;
+    double* A = scr + 64;
+    double* A2 = scr + 128;
+    double* A4 = scr + 192;
+    double* A6 = scr + 256;
+    double* T1 = scr + 320;
+    double* T2 = scr + 384;
+    double* U = scr + 448;
+    double* Vv = scr + 512;
+    const double b[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
+                          1187353796428800.0,  129060195264000.0,   10559470521600.0,
+                          670442572800.0,      33522128640.0,       1323241920.0,
+                          40840800.0,          960960.0,            16380.0,
+                          182.0,               1.0};
+    const double theta13 = 5.371920351148152;
+    // 1-norm and scaling exponent
+    double cs = 0.0;
+    if (act) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) cs += fabs(M[r * 8 + j]);
+    }
+    const double nrm = wave_max(cs);
+    int s = 0;
+    if (nrm > theta13) s = (int)ceil(log2(nrm / theta13));
+    if (act) A[lane] = ldexp(M[lane], -s);
+    // squaring count must be uniform across the workgroup (barriers below)
+    if (lane == 0) red[threadIdx.x >> 6] = act ? (double)s : 0.0;
+    __syncthreads();
+    int smax = 0;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) smax = max(smax, (int)red[ww]);
+    if (act) A2[lane] = mm_entry(A, A, i, j);
+    __syncthreads();
+    if (act) A4[lane] = mm_entry(A2, A2, i, j);
+    __syncthreads();
+    if (act) A6[lane] = mm_entry(A4, A2, i, j);
+    __syncthreads();
+    if (act) {
+        T1[lane] = b[13] * A6[lane] + b[11] * A4[lane] + b[9] * A2[lane];
+        T2[lane] = b[12] * A6[lane] + b[10] * A4[lane] + b[8] * A2[lane];
+    }
+    __syncthreads();
+    const double id = (i == j) ? 1.0 : 0.0;
+    if (act) {
+        U[lane] = mm_entry(A6, T1, i, j) + b[7] * A6[lane] + b[5] * A4[lane] + b[3] * A2[lane] +
+                  b[1] * id;
+        Vv[lane] = mm_entry(A6, T2, i, j) + b[6] * A6[lane] + b[4] * A4[lane] + b[2] * A2[lane] +
+                   b[0] * id;
+    }
+    __syncthreads();
+    if (act) T1[lane] = mm_entry(A, U, i, j);   // U = A * U2
+    __syncthreads();
+    // augmented [V-U | V+U] (8 x 16) in aug = scr[0..127]
+    double* aug = scr;
+    if (act) {
+        aug[i * 16 + j] = Vv[lane] - T1[lane];
+        aug[i * 16 + 8 + j] = Vv[lane] + T1[lane];
+    }
+    __syncthreads();
+    // Gauss-Jordan with partial pivoting
+    for (int k = 0; k < 8; ++k) {
+        double key = -1.0;
+        if (act && lane < 8 && lane >= k) key = fabs(aug[lane * 16 + k]);
+        // argmax over lanes: pack (key, lane) by comparing
+        double best = wave_max(key);
+        unsigned long long ball = __ballot(act && lane < 8 && lane >= k && key == best);
+        int p = ball ? __ffsll((long long)ball) - 1 : k;
+        __syncthreads();
+        if (act && p != k && lane < 16) {
+            double t0 = aug[k * 16 + lane];
+            aug[k * 16 + lane] = aug[p * 16 + lane];
+            aug[p * 16 + lane] = t0;
+        }
+        __syncthreads();
+        double nv0 = 0.0, nv1 = 0.0;
+        if (act) {
+            const double piv = aug[k * 16 + k];
+            const double fi = aug[i * 16 + k];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int c = j + 8 * h;
+                double val = aug[i * 16 + c];
+                if (i == k)
+                    val = val / piv;
+                else
+                    val = val - fi * (aug[k * 16 + c] / piv);
+                if (h == 0) nv0 = val; else nv1 = val;
+            }
+        }
+        __syncthreads();
+        if (act) {
+            aug[i * 16 + j] = nv0;
+            aug[i * 16 + 8 + j] = nv1;
+        }
+        __syncthreads();
+    }
+    // X = aug[:, 8:16] -> A (aliases aug rows 4..7: read, barrier, write); square s times
+    {
+        const double xv = act ? aug[i * 16 + 8 + j] : 0.0;
+        __syncthreads();
+        if (act) A[lane] = xv;
+        __syncthreads();
+    }
+    for (int q = 0; q < smax; ++q) {
+        const bool sq = act && q < s;
+        double v = sq ? mm_entry(A, A, i, j) : 0.0;
+        __syncthreads();
+        if (sq) A[lane] = v;
+        __syncthreads();
+    }
+    // result in A (= scr + 64)
+}
+
+// ---------------------------------------------------------------------------
+// Problem setup: inputs, reference sampling, per-vehicle linearisation
+// (MPCclass, MPC_Iter.py:59-149), scaled cost gradient, row table.
+// Returns sampler flag.
+// ---------------------------------------------------------------------------
+__device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) {
+    const int tid = threadIdx.x, V = L.V, O = L.O, Hb = L.Hb, Hm = P.hpMax;
+    for (int i = tid; i < 6 * V; i += NT) L.x0[i] = a.x0[(size_t)b * V * 6 + i];
+    for (int i = tid; i < V; i += NT) L.u0[i] = a.u0 ? a.u0[(size_t)b * V + i] : 0.0;
+    for (int i = tid; i < 2 * V; i += NT) L.ec[i] = a.ec ? a.ec[(size_t)b * V * 2 + i] : 0.0;
+    for (int i = tid; i < O * 2 * Hb; i += NT) {
+        const int o = i / (2 * Hb), c = (i / Hb) & 1, k = i % Hb;
+        L.ob[(o * Hb + k) * 2 + c] = a.obst[(size_t)b * O * 2 * Hm + i];
+    }
+    __syncthreads();
+    int sflag = 0;
+    if (a.refIn) {
+        for (int i = tid; i < Hb * 2 * V; i += NT) {
+            const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
+            L.ref[(v * Hb + k) * 2 + c] = a.refIn[(size_t)b * Hm * 2 * V + i];
+        }
+    } else if (tid < V) {
+        const double* xv = L.x0 + 6 * tid;
+        sflag = sample_reference(P, tid, xv[0], xv[1], xv[3] * P.dt, Hb, L.ref + tid * Hb * 2);
+    }
+    __syncthreads();
+    if (a.mode == MODE_SAMPLE) return sflag;
+
+    // per-vehicle linearisation, one wave per vehicle per round
+    const int w = tid >> 6, lane = tid & 63;
+    for (int r0 = 0; r0 < V; r0 += NWAVE) {
+        const int v = r0 + w;
+        const bool act = v < V;
+        double* scr = L.scr + w * SCR_PER_WAVE;
+        if (act) {
+            double Ac[6][6], Ec[6];
+            bicycle_jacobian(L.x0 + 6 * v, L.u0[v], P.Lf[v], P.Lr[v], L.ec[2 * v], L.ec[2 * v + 1],
+                             Ac, Ec);
+            const int i = lane >> 3, j = lane & 7;
+            double mv = 0.0;
+            if (i < 6) {
+                if (j < 6) {
+                    // static indexing into Ac via unrolled select
+#pragma unroll
+                    for (int ii = 0; ii < 6; ++ii)
+#pragma unroll
+                        for (int jj = 0; jj < 6; ++jj)
+                            if (ii == i && jj == j) mv = Ac[ii][jj];
+                } else if (j == 6) {
+                    mv = (i == 5) ? 10.0 : 0.0;
+                } else {
+#pragma unroll
+                    for (int ii = 0; ii < 6; ++ii)
+                        if (ii == i) mv = Ec[ii];
+                }
+            }
+            scr[lane] = P.dt * mv;
+        }
+        __syncthreads();
+        expm8(scr, act, L.red);
+        // Ad = X[0:6,0:6], Bd = X[0:6,6], Ed = X[0:6,7] (threshold 1e-30, MPC_Iter.py:87)
+        double adrow[6];
+        double bi = 0.0, ei = 0.0, xi = 0.0;
+        const double* X = scr + 64;
+        const int comp = lane < 8 ? lane : lane - 8;   // lanes 0..5: state recursion, 8..13: impulse
+        if (act && comp < 6 && lane < 16) {
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) adrow[jj] = X[comp * 8 + jj];
+            bi = X[comp * 8 + 6];
+            ei = X[comp * 8 + 7];
+            if (fabs(ei) <= 1e-30) ei = 0.0;
+            xi = L.x0[6 * v + comp];
+        } else {
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) adrow[jj] = 0.0;
+        }
+        if (act && a.mode == MODE_LINEARIZE && lane < 6) {
+            const size_t base = ((size_t)b * V + v);
+            if (a.Ad)
+                for (int jj = 0; jj < 6; ++jj) a.Ad[base * 36 + lane * 6 + jj] = adrow[jj];
+            if (a.Bd) a.Bd[base * 6 + lane] = bi;
+            if (a.Ed) a.Ed[base * 6 + lane] = ei;
+        }
+        // recursions: x_{k+1} = Ad x_k + Ed  (p0_k = C x_{k+1});  b_{m+1} = Ad b_m (g_m = C b_m)
+        double cur = (lane < 8) ? xi : bi;
+        const double add = (lane < 8) ? ei : 0.0;
+        const int base = lane < 8 ? 0 : 8;
+        for (int k = 0; k < Hb; ++k) {
+            if (lane >= 8 && lane < 14 && act && comp < 2) L.g[(v * Hb + k) * 2 + comp] = cur;
+            double nxt = add;
+#pragma unroll
+            for (int jj = 0; jj < 6; ++jj) nxt += adrow[jj] * __shfl(cur, base + jj, 64);
+            if (lane < 8) cur = nxt;
+            if (lane >= 8) cur = nxt;
+            if (lane < 2 && act) L.p0[(v * Hb + k) * 2 + lane] = cur;
+        }
+        __syncthreads();
+    }
+    // scaled cost gradient  qs = uLim * Psi0,  Psi0 = -2 calB' Q (ref - const)  (MPC_Iter.py:125)
+    for (int e = tid; e < V * Hb; e += NT) {
+        const int v = e / Hb, l = e % Hb;
+        double acc = 0.0;
+        for (int k = l; k < Hb; ++k) {
+            const double qk = (k == Hb - 1) ? P.Qf[v] : P.Q[v];
+            const double* gg = L.g + (v * Hb + k - l) * 2;
+            const double ex = L.ref[(v * Hb + k) * 2] - L.p0[(v * Hb + k) * 2];
+            const double ey = L.ref[(v * Hb + k) * 2 + 1] - L.p0[(v * Hb + k) * 2 + 1];
+            acc += qk * (gg[0] * ex + gg[1] * ey);
+        }
+        L.qs[e] = P.uLim * (-2.0 * acc);
+    }
+    // row table
+    for (int r = tid; r < L.m; r += NT) {
+        int i, j, o, k;
+        if (r < L.mp) {
+            const int pi = r / Hb;
+            k = r % Hb;
+            int ii = 0, rem = pi;
+            while (rem >= V - 1 - ii) { rem -= V - 1 - ii; ++ii; }
+            i = ii;
+            j = ii + 1 + rem;
+            o = -1;
+        } else {
+            const int ro = r - L.mp;
+            const int vo = ro / Hb;
+            k = ro % Hb;
+            i = vo / O;
+            o = vo % O;
+            j = -1;
+        }
+        L.rinfo[r] = i | ((j + 1) << 8) | ((o + 1) << 16) | (k << 24);
+    }
+    __syncthreads();
+    return sflag;
+}
+
+// ---------------------------------------------------------------------------
+// Structured linear operators (y-space = predicted-position space, [V][Hb][2])
+// ---------------------------------------------------------------------------
+// y[v][k] = sum_{l<=k} g[v][k-l] * x[v*Hb + l]     (calB x, MPC_Iter.py:146-147)
+__device__ __forceinline__ void toeplitz_apply(const Lay& L, const double* x, double* y) {
+    for (int e = threadIdx.x; e < L.V * L.Hb; e += NT) {
+        const int v = e / L.Hb, k = e % L.Hb;
+        const double* gv = L.g + v * L.Hb * 2;
+        const double* xv = x + v * L.Hb;
+        double a0 = 0.0, a1 = 0.0;
+        for (int l = 0; l <= k; ++l) {
+            a0 += gv[(k - l) * 2] * xv[l];
+            a1 += gv[(k - l) * 2 + 1] * xv[l];
+        }
+        y[2 * e] = a0;
+        y[2 * e + 1] = a1;
+    }
+}
+
+// out[v*Hb+l] = sum_{k>=l} g[v][k-l]' y[v][k]        (calB' y)
+__device__ __forceinline__ double toeplitz_t_entry(const Lay& L, const double* y, int v, int l) {
+    const double* gv = L.g + v * L.Hb * 2;
+    const double* yv = y + v * L.Hb * 2;
+    double acc = 0.0;
+    for (int k = l; k < L.Hb; ++k) acc += gv[(k - l) * 2] * yv[2 * k] + gv[(k - l) * 2 + 1] * yv[2 * k + 1];
+    return acc;
+}
+
+// sum over the rows incident to (v, k) of coef(r) * sigma * e_r  (2-vector)
+template <class F>
+__device__ __forceinline__ void incident_sum(const Lay& L, int v, int k, F coef, double& s0,
+                                            double& s1) {
+    s0 = 0.0;
+    s1 = 0.0;
+    for (int w = 0; w < L.V; ++w) {
+        if (w == v) continue;
+        const int i = v < w ? v : w, j = v < w ? w : v;
+        const int r = pair_index(i, j, L.V) * L.Hb + k;
+        const double c = (v == i ? -1.0 : 1.0) * coef(r);
+        s0 += c * L.rowE[2 * r];
+        s1 += c * L.rowE[2 * r + 1];
+    }
+    for (int o = 0; o < L.O; ++o) {
+        const int r = L.mp + (v * L.O + o) * L.Hb + k;
+        const double c = -coef(r);
+        s0 += c * L.rowE[2 * r];
+        s1 += c * L.rowE[2 * r + 1];
+    }
+}
+
+// Phase 2 of G x (needs ya = calB x_u):  out[i] = (G x)_i  (+ add[i] - h_i if given)
+__device__ __forceinline__ double gx_row(const Lay& L, const double* ya, const double* xu,
+                                         double xw, int r) {
+    if (r < L.m) {
+        int i, j, o, k;
+        row_decode(L, L.rinfo[r], i, j, o, k);
+        const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1];
+        double val = -(e0 * ya[(i * L.Hb + k) * 2] + e1 * ya[(i * L.Hb + k) * 2 + 1]);
+        if (j >= 0) val += e0 * ya[(j * L.Hb + k) * 2] + e1 * ya[(j * L.Hb + k) * 2 + 1];
+        return val + L.rowW[r] * xw;
+    }
+    if (r < L.m + L.N) return xu[r - L.m];
+    if (r < L.m + 2 * L.N) return -xu[r - L.m - L.N];
+    return -xw;
+}
+
+// G' t: u-part into out[0..N), omega part returned (uniform).  Two phases.
+__device__ double gt_apply(const Lay& L, const double* t, double* out) {
+    const int tid = threadIdx.x;
+    double wsum = 0.0;
+    for (int e = tid; e < L.V * L.Hb; e += NT) {
+        const int v = e / L.Hb, k = e % L.Hb;
+        double s0, s1;
+        incident_sum(L, v, k, [&](int r) { return t[r]; }, s0, s1);
+        L.yb[2 * e] = s0;
+        L.yb[2 * e + 1] = s1;
+    }
+    for (int r = tid; r < L.m; r += NT) wsum += t[r] * L.rowW[r];
+    double red[4] = {wsum, 0.0, 0.0, 0.0};
+    block_reduce4(red, 0, L.red);   // includes barriers: yb visible afterwards
+    for (int e = tid; e < L.N; e += NT) {
+        const int v = e / L.Hb, l = e % L.Hb;
+        out[e] = toeplitz_t_entry(L, L.yb, v, l) + t[L.m + e] - t[L.m + L.N + e];
+    }
+    return red[0] - t[L.mc - 1];
+}
+
+// ---------------------------------------------------------------------------
+// Normal matrix assembly  K = P_s + rho I + G' diag(d) G   (lower triangle)
+// ---------------------------------------------------------------------------
+template <bool HG>
+__device__ void assemble(const DevParams& P, const Lay& L, const double* d, double rho) {
+    const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb;
+    const double u2 = P.uLim * P.uLim;
+    // phase 1: W~ blocks [k][a>=b] (2x2) and the omega-coupling vector in y-space (yb)
+    const int nW = Hb * nb;
+    for (int e = tid; e < nW + V * Hb; e += NT) {
+        if (e < nW) {
+            const int k = e / nb, ab = e % nb;
+            int a_ = 0;
+            while ((a_ + 1) * (a_ + 2) / 2 <= ab) ++a_;
+            const int b_ = ab - a_ * (a_ + 1) / 2;
+            double w00 = 0.0, w01 = 0.0, w10 = 0.0, w11 = 0.0;
+            if (a_ == b_) {
+                const double qk = 2.0 * u2 * ((k == Hb - 1) ? P.Qf[a_] : P.Q[a_]);
+                w00 = qk;
+                w11 = qk;
+                for (int wv = 0; wv < V; ++wv) {
+                    if (wv == a_) continue;
+                    const int i = a_ < wv ? a_ : wv, j = a_ < wv ? wv : a_;
+                    const int r = pair_index(i, j, V) * Hb + k;
+                    const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1], dr = d[r];
+                    w00 += dr * e0 * e0;
+                    w01 += dr * e0 * e1;
+                    w11 += dr * e1 * e1;
+                }
+                for (int o = 0; o < L.O; ++o) {
+                    const int r = L.mp + (a_ * L.O + o) * Hb + k;
+                    const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1], dr = d[r];
+                    w00 += dr * e0 * e0;
+                    w01 += dr * e0 * e1;
+                    w11 += dr * e1 * e1;
+                }
+                w10 = w01;
+            } else {
+                const int r = pair_index(b_, a_, V) * Hb + k;   // b_ < a_
+                const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1], dr = -d[r];
+                w00 = dr * e0 * e0;
+                w01 = dr * e0 * e1;
+                w10 = w01;
+                w11 = dr * e1 * e1;
+            }
+            double* W = L.Wt + 4 * e;
+            W[0] = w00; W[1] = w01; W[2] = w10; W[3] = w11;
+        } else {
+            const int q = e - nW, v = q / Hb, k = q % Hb;
+            double s0, s1;
+            incident_sum(L, v, k, [&](int r) { return d[r] * L.rowW[r]; }, s0, s1);
+            L.yb[2 * q] = s0;
+            L.yb[2 * q + 1] = s1;
+        }
+    }
+    double ww = 0.0;
+    for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
+    double red[4] = {ww, 0.0, 0.0, 0.0};
+    block_reduce4(red, 0, L.red);
+    // phase 2: K_uu lower triangle, omega row, omega diagonal
+    const int N = L.N, ld = L.ld;
+    double* H = L.H;
+    const int ty = tid >> 4, tx = tid & 15;
+    for (int row = ty; row < N; row += 16) {
+        const int a_ = row / Hb, l = row % Hb;
+        const double* ga = L.g + a_ * Hb * 2;
+        for (int col = tx; col <= row; col += 16) {
+            const int b_ = col / Hb, lp = col % Hb;
+            const double* gb = L.g + b_ * Hb * 2;
+            const int k0 = l > lp ? l : lp;
+            const double* W = L.Wt + 4 * (k0 * nb + a_ * (a_ + 1) / 2 + b_);
+            double acc = 0.0;
+            for (int k = k0; k < Hb; ++k, W += 4 * nb) {
+                const double gb0 = gb[(k - lp) * 2], gb1 = gb[(k - lp) * 2 + 1];
+                const double t0 = W[0] * gb0 + W[1] * gb1;
+                const double t1 = W[2] * gb0 + W[3] * gb1;
+                acc += ga[(k - l) * 2] * t0 + ga[(k - l) * 2 + 1] * t1;
+            }
+            if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
+            H[row * ld + col] = acc;
+        }
+    }
+    for (int e = tid; e < N; e += NT) {
+        const int v = e / Hb, l = e % Hb;
+        H[N * ld + e] = toeplitz_t_entry(L, L.yb, v, l);
+    }
+    if (tid == 0) H[N * ld + N] = red[0] + d[L.mc - 1] + rho;
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Cholesky  K = L L'  in place (lower), right-looking, one barrier per column
+// (column j-1 is scaled during step j).  Returns false on a non-positive pivot.
+// dinv[j] = 1 / L_jj.
+// ---------------------------------------------------------------------------
+template <bool HG>
+__device__ bool cholesky(const Lay& L) {
+    const int tid = threadIdx.x, n = L.n, ld = L.ld;
+    double* H = L.H;
+    const int ty = tid >> 4, tx = tid & 15;
+    for (int j = 0; j < n; ++j) {
+        const double piv = H[j * ld + j];
+        if (!(piv > 0.0) || !isfinite(piv)) {
+            __syncthreads();
+            return false;
+        }
+        if (j > 0) {
+            const double sc = L.dinv[j - 1];
+            for (int i = j + tid; i < n; i += NT) H[i * ld + j - 1] *= sc;
+        }
+        const double rp = 1.0 / piv;
+        for (int i = j + 1 + ty; i < n; i += 16) {
+            const double lij = H[i * ld + j] * rp;
+            for (int k = j + 1 + tx; k <= i; k += 16) H[i * ld + k] -= lij * H[k * ld + j];
+        }
+        if (tid == 0) L.dinv[j] = 1.0 / sqrt(piv);
+        __syncthreads();
+    }
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Triangular solves with the factor: x = K^{-1} b.  Wave 0 only (column /
+// row oriented, pivots broadcast with v_readlane); rows i = lane + 64 t.
+// ---------------------------------------------------------------------------
+template <bool HG>
+__device__ void chol_solve(const Lay& L, const double* bvec, double* x) {
+    const int tid = threadIdx.x;
+    if (tid < 64) {
+        const int lane = tid, n = L.n, ld = L.ld;
+        const double* H = L.H;
+        double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+        if (lane < n) r0 = bvec[lane];
+        if (lane + 64 < n) r1 = bvec[lane + 64];
+        if (lane + 128 < n) r2 = bvec[lane + 128];
+        if (lane + 192 < n) r3 = bvec[lane + 192];
+        // forward: L y = b  (scaled column j is H[i][j] * dinv[j]; H holds L below the diagonal)
+        for (int j = 0; j < n; ++j) {
+            const int t = j >> 6, ln = j & 63;
+            double bj = (t == 0) ? r0 : (t == 1) ? r1 : (t == 2) ? r2 : r3;
+            const double xj = readlane_d(bj, ln) * L.dinv[j];
+            if (lane == ln) {
+                if (t == 0) r0 = xj; else if (t == 1) r1 = xj; else if (t == 2) r2 = xj; else r3 = xj;
+            }
+            const int i0 = lane, i1 = lane + 64, i2 = lane + 128, i3 = lane + 192;
+            if (i0 > j && i0 < n) r0 -= H[i0 * ld + j] * xj;
+            if (i1 > j && i1 < n) r1 -= H[i1 * ld + j] * xj;
+            if (i2 > j && i2 < n) r2 -= H[i2 * ld + j] * xj;
+            if (i3 > j && i3 < n) r3 -= H[i3 * ld + j] * xj;
+        }
+        // backward: L' x = y
+        for (int j = n - 1; j >= 0; --j) {
+            const int t = j >> 6, ln = j & 63;
+            double bj = (t == 0) ? r0 : (t == 1) ? r1 : (t == 2) ? r2 : r3;
+            const double xj = readlane_d(bj, ln) * L.dinv[j];
+            if (lane == ln) {
+                if (t == 0) r0 = xj; else if (t == 1) r1 = xj; else if (t == 2) r2 = xj; else r3 = xj;
+            }
+            const double* Lr = H + j * ld;
+            if (lane < j) r0 -= Lr[lane] * xj;
+            if (lane + 64 < j) r1 -= Lr[lane + 64] * xj;
+            if (lane + 128 < j) r2 -= Lr[lane + 128] * xj;
+            if (lane + 192 < j) r3 -= Lr[lane + 192] * xj;
+        }
+        if (lane < n) x[lane] = r0;
+        if (lane + 64 < n) x[lane + 64] = r1;
+        if (lane + 128 < n) x[lane + 128] = r2;
+        if (lane + 192 < n) x[lane + 192] = r3;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// QCQP evaluation (SCP_controller.py:215-265) of the unscaled control vector u
+// (LDS, [V*Hb]).  Positions go to L.pb.  Obstacle rows follow quirk B.4 when
+// flagged: evaluated (nVeh-1-v) times (sum) and never for the last vehicle.
+// ---------------------------------------------------------------------------
+struct EvalRes {
+    double obj, maxv, sumv;
+    int feasible;
+};
+
+__device__ EvalRes evaluate_u(const DevParams& P, const Lay& L, const double* u, double* cveh,
+                              double* cobs) {
+    const int tid = threadIdx.x, V = L.V, Hb = L.Hb, O = L.O;
+    toeplitz_apply(L, u, L.pb);
+    __syncthreads();
+    for (int e = tid; e < V * Hb; e += NT) {
+        L.pb[2 * e] += L.p0[2 * e];
+        L.pb[2 * e + 1] += L.p0[2 * e + 1];
+    }
+    __syncthreads();
+    double obj = 0.0, mx = 0.0, sm = 0.0, nviol = 0.0;
+    for (int e = tid; e < V * Hb; e += NT) {
+        const int v = e / Hb, k = e % Hb;
+        const double qk = (k == Hb - 1) ? P.Qf[v] : P.Q[v];
+        const double ex = L.pb[2 * e] - L.ref[2 * e], ey = L.pb[2 * e + 1] - L.ref[2 * e + 1];
+        obj += qk * (ex * ex + ey * ey) + P.R[v] * u[e] * u[e];
+    }
+    const bool quirk = (P.flags & SCPQP_FLAG_OBST_QUIRK) != 0;
+    for (int r = tid; r < L.m; r += NT) {
+        int i, j, o, k;
+        row_decode(L, L.rinfo[r], i, j, o, k);
+        const double* pi = L.pb + (i * Hb + k) * 2;
+        double dx, dy, D2;
+        if (j >= 0) {
+            dx = pi[0] - L.pb[(j * Hb + k) * 2];
+            dy = pi[1] - L.pb[(j * Hb + k) * 2 + 1];
+            D2 = P.D2veh[i * SCPQP_MAX_VEH + j];
+        } else {
+            dx = pi[0] - L.ob[(o * Hb + k) * 2];
+            dy = pi[1] - L.ob[(o * Hb + k) * 2 + 1];
+            D2 = P.D2obs[i * SCPQP_MAX_OBST + o];
+        }
+        const double c = D2 - (dx * dx + dy * dy);
+        int reps = 1;
+        if (j < 0 && quirk) reps = V - 1 - i;
+        if (cveh && j >= 0) {
+            cveh[(i * V + j) * Hb + k] = c;
+            cveh[(j * V + i) * Hb + k] = c;
+        }
+        if (cobs && j < 0 && reps > 0) cobs[(i * O + o) * Hb + k] = c;
+        if (c > P.ctol && reps > 0) {
+            mx = fmax(mx, c);
+            sm += c * reps;
+            nviol += 1.0;
+        }
+    }
+    double red[4] = {obj, sm, nviol, mx};
+    block_reduce4(red, 8, L.red);
+    EvalRes res;
+    res.obj = red[0];
+    res.sumv = red[1];
+    res.feasible = red[2] == 0.0;
+    res.maxv = red[3];
+    return res;
+}
+
+// ---------------------------------------------------------------------------
+// Constraint linearisation at u-bar = L.ub (SCP_controller.py:93-128 in the
+// factored form of SURVEY A.5), scaled rows:
+//   e_r = 2 d uLim / nrm,  w_r = -1/nrm,  h_r = b_r / nrm,
+//   nrm = || [a_r uLim, -1] ||,  a_r = -2 d' calB_i,k (+ 2 d' calB_j,k)
+// ---------------------------------------------------------------------------
+__device__ void linearise_rows(const DevParams& P, const Lay& L) {
+    const int tid = threadIdx.x, Hb = L.Hb;
+    toeplitz_apply(L, L.ub, L.ya);
+    __syncthreads();
+    for (int e = tid; e < L.V * Hb; e += NT) {
+        L.pb[2 * e] = L.p0[2 * e] + L.ya[2 * e];
+        L.pb[2 * e + 1] = L.p0[2 * e + 1] + L.ya[2 * e + 1];
+    }
+    __syncthreads();
+    for (int r = tid; r < L.m; r += NT) {
+        int i, j, o, k;
+        row_decode(L, L.rinfo[r], i, j, o, k);
+        const double* pi = L.pb + (i * Hb + k) * 2;
+        const double* yi = L.ya + (i * Hb + k) * 2;
+        double dx, dy, D2, au;
+        if (j >= 0) {
+            dx = pi[0] - L.pb[(j * Hb + k) * 2];
+            dy = pi[1] - L.pb[(j * Hb + k) * 2 + 1];
+            D2 = P.D2veh[i * SCPQP_MAX_VEH + j];
+            const double* yj = L.ya + (j * Hb + k) * 2;
+            au = -2.0 * (dx * yi[0] + dy * yi[1]) + 2.0 * (dx * yj[0] + dy * yj[1]);
+        } else {
+            dx = pi[0] - L.ob[(o * Hb + k) * 2];
+            dy = pi[1] - L.ob[(o * Hb + k) * 2 + 1];
+            D2 = P.D2obs[i * SCPQP_MAX_OBST + o];
+            au = -2.0 * (dx * yi[0] + dy * yi[1]);
+        }
+        const double c = D2 - (dx * dx + dy * dy);
+        const double brow = -c + au;
+        double a2 = 0.0;
+        const double* gi = L.g + i * Hb * 2;
+        for (int l = 0; l <= k; ++l) {
+            const double t = dx * gi[(k - l) * 2] + dy * gi[(k - l) * 2 + 1];
+            a2 += t * t;
+        }
+        if (j >= 0) {
+            const double* gj = L.g + j * Hb * 2;
+            for (int l = 0; l <= k; ++l) {
+                const double t = dx * gj[(k - l) * 2] + dy * gj[(k - l) * 2 + 1];
+                a2 += t * t;
+            }
+        }
+        const double nrm = sqrt(4.0 * a2 * P.uLim * P.uLim + 1.0);
+        L.rowE[2 * r] = 2.0 * dx * P.uLim / nrm;
+        L.rowE[2 * r + 1] = 2.0 * dy * P.uLim / nrm;
+        L.rowW[r] = -1.0 / nrm;
+        L.rowH[r] = brow / nrm;
+    }
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// QP: Mehrotra predictor-corrector IPM + active-set polish, scaled variables.
+// x = L.z = [u~ (N), omega].  Returns IPM iterations; sets *qflags.
+// ---------------------------------------------------------------------------
+// G x  -> out (mc), phase structure: toeplitz into ya, then rows.
+__device__ void g_apply(const Lay& L, const double* x, double* out, const double* add_s,
+                        bool minus_h) {
+    toeplitz_apply(L, x, L.ya);
+    __syncthreads();
+    const double xw = x[L.N];
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        double val = gx_row(L, L.ya, x, xw, r);
+        if (add_s) val += add_s[r];
+        if (minus_h) val -= hval(L, r);
+        out[r] = val;
+    }
+    __syncthreads();
+}
+
+// residuals rd (n), rp (mc) at (z, s, lam); returns {max|rp|, max|rd|, gap, pobj}
+__device__ void residuals(const DevParams& P, const Lay& L, double out[4]) {
+    const int tid = threadIdx.x, N = L.N, Hb = L.Hb;
+    const double u2 = P.uLim * P.uLim;
+    toeplitz_apply(L, L.z, L.ya);
+    __syncthreads();
+    const double zw = L.z[N];
+    double mrp = 0.0, gap = 0.0, wl = 0.0, quad = 0.0;
+    for (int r = tid; r < L.mc; r += NT) {
+        const double v = gx_row(L, L.ya, L.z, zw, r) + L.s[r] - hval(L, r);
+        L.rp[r] = v;
+        mrp = fmax(mrp, fabs(v));
+        gap += L.s[r] * L.lam[r];
+        if (r < L.m) wl += L.lam[r] * L.rowW[r];
+    }
+    for (int e = tid; e < L.V * Hb; e += NT) {
+        const int v = e / Hb, k = e % Hb;
+        const double qk = 2.0 * u2 * ((k == Hb - 1) ? P.Qf[v] : P.Q[v]);
+        double s0, s1;
+        incident_sum(L, v, k, [&](int r) { return L.lam[r]; }, s0, s1);
+        const double y0 = L.ya[2 * e], y1 = L.ya[2 * e + 1];
+        L.yb[2 * e] = qk * y0 + s0;
+        L.yb[2 * e + 1] = qk * y1 + s1;
+        quad += qk * (y0 * y0 + y1 * y1);
+    }
+    double red[4] = {mrp, gap, wl, quad};
+    block_reduce4(red, 1, L.red);
+    double mrd = 0.0, quad2 = 0.0, lin = 0.0;
+    for (int e = tid; e < N; e += NT) {
+        const int v = e / Hb, l = e % Hb;
+        const double ze = L.z[e];
+        const double pu = 2.0 * u2 * P.R[v] * ze;
+        const double v_ = toeplitz_t_entry(L, L.yb, v, l) + pu + L.qs[e] + L.lam[L.m + e] -
+                          L.lam[L.m + N + e];
+        L.rd[e] = v_;
+        mrd = fmax(mrd, fabs(v_));
+        quad2 += pu * ze;
+        lin += L.qs[e] * ze;
+    }
+    const double rdw = P.slackW + red[2] - L.lam[L.mc - 1];
+    if (tid == 0) L.rd[N] = rdw;
+    double red2[4] = {mrd, quad2, lin, 0.0};
+    block_reduce4(red2, 1, L.red);
+    out[0] = red[0];
+    out[1] = fmax(red2[0], fabs(rdw));
+    out[2] = red[1];
+    out[3] = 0.5 * (red[3] + red2[1]) + red2[2] + P.slackW * zw;
+}
+
+// max step keeping s + a ds >= 0, lam + a dl >= 0 (capped at 1)
+__device__ double max_step(const Lay& L) {
+    double a = 1.0;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        if (L.ds[r] < 0.0) a = fmin(a, -L.s[r] / L.ds[r]);
+        if (L.dl[r] < 0.0) a = fmin(a, -L.lam[r] / L.dl[r]);
+    }
+    double red[4] = {-a, 0.0, 0.0, 0.0};
+    block_reduce4(red, 1, L.red);
+    return -red[0];
+}
+
+// Newton direction for complementarity target rc (given through rc_of(r)):
+//   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
+template <bool HG, class RC>
+__device__ void newton_dir(const Lay& L, RC rc_of) {
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.dd[r] * L.rp[r] - rc_of(r) / L.s[r];
+    __syncthreads();
+    const double ow = gt_apply(L, L.tv, L.rhs);
+    if (threadIdx.x == 0) L.rhs[L.N] = ow;
+    __syncthreads();
+    for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
+    __syncthreads();
+    chol_solve<HG>(L, L.rhs, L.dz);
+    g_apply(L, L.dz, L.ds, nullptr, false);
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        const double dsr = -L.rp[r] - L.ds[r];
+        L.ds[r] = dsr;
+        L.dl[r] = -(rc_of(r) + L.lam[r] * dsr) / L.s[r];
+    }
+    __syncthreads();
+}
+
+template <bool HG>
+__device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
+    const int tid = threadIdx.x, n = L.n, mc = L.mc, N = L.N;
+    // ---- scale factors of the termination test
+    double hmax = 1.0;
+    for (int r = tid; r < L.m; r += NT) hmax = fmax(hmax, fabs(L.rowH[r]));
+    double qmax = fmax(1.0, P.slackW);
+    for (int e = tid; e < N; e += NT) qmax = fmax(qmax, fabs(L.qs[e]));
+    {
+        double red[4] = {hmax, qmax, 0.0, 0.0};
+        block_reduce4(red, 3, L.red);
+        hmax = red[0];
+        qmax = red[1];
+    }
+    // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
+    for (int r = tid; r < mc; r += NT) {
+        L.dd[r] = 1.0;
+        L.tv[r] = hval(L, r);
+    }
+    __syncthreads();
+    assemble<HG>(P, L, L.dd, 0.0);
+    cholesky<HG>(L);   // P + G'G is positive definite (box and omega rows)
+    {
+        const double ow = gt_apply(L, L.tv, L.rhs);
+        if (tid == 0) L.rhs[N] = ow - P.slackW;
+        __syncthreads();
+        for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e];
+        __syncthreads();
+        chol_solve<HG>(L, L.rhs, L.z);
+    }
+    g_apply(L, L.z, L.s, nullptr, false);
+    double smin = 1e300, ssq = 0.0;
+    for (int r = tid; r < mc; r += NT) {
+        const double sv = hval(L, r) - L.s[r];
+        L.s[r] = sv;
+        L.lam[r] = -sv;
+        smin = fmin(smin, sv);
+        ssq += sv * sv;
+    }
+    {
+        double red[4] = {-smin, ssq, 0.0, 0.0};
+        block_reduce4(red, 1, L.red);
+        const double ts = red[0], nrm = sqrt(red[1]);
+        // s shift (ts = -min s) and lam shift (tz = -min lam = max s)
+        double smax = -1e300;
+        for (int r = tid; r < mc; r += NT) smax = fmax(smax, -L.lam[r]);
+        double red2[4] = {smax, 0.0, 0.0, 0.0};
+        block_reduce4(red2, 1, L.red);
+        const double tz = red2[0];
+        const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
+        const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
+        for (int r = tid; r < mc; r += NT) {
+            if (shs) L.s[r] += 1.0 + ts;
+            if (shz) L.lam[r] += 1.0 + tz;
+        }
+        __syncthreads();
+    }
+    // ---- Mehrotra iterations
+    int it = 0;
+    bool conv = false;
+    for (; it < P.maxIpm; ++it) {
+        double res[4];
+        residuals(P, L, res);
+        if (res[0] <= P.ipmTol * hmax && res[1] <= P.ipmTol * qmax &&
+            res[2] <= P.ipmTol * fmax(1.0, fabs(res[3]))) {
+            conv = true;
+            break;
+        }
+        const double mu = res[2] / mc;
+        for (int r = tid; r < mc; r += NT) L.dd[r] = L.lam[r] / L.s[r];
+        __syncthreads();
+        assemble<HG>(P, L, L.dd, 0.0);
+        if (!cholesky<HG>(L)) break;
+        // predictor (affine scaling): rc = s lam
+        newton_dir<HG>(L, [&](int r) { return L.s[r] * L.lam[r]; });
+        double aaff = max_step(L);
+        double mua = 0.0;
+        for (int r = tid; r < mc; r += NT) {
+            mua += (L.s[r] + aaff * L.ds[r]) * (L.lam[r] + aaff * L.dl[r]);
+            L.sa[r] = L.ds[r];
+            L.la[r] = L.dl[r];
+        }
+        double red[4] = {mua, 0.0, 0.0, 0.0};
+        block_reduce4(red, 0, L.red);
+        const double sr = red[0] / mc / mu;
+        const double sigma = sr * sr * sr;
+        const double smu = sigma * mu;
+        // corrector: rc = s lam + ds_aff dl_aff - sigma mu
+        newton_dir<HG>(L, [&](int r) { return L.s[r] * L.lam[r] + L.sa[r] * L.la[r] - smu; });
+        const double alpha = fmin(1.0, 0.99 * max_step(L));
+        for (int e = tid; e < n; e += NT) L.z[e] += alpha * L.dz[e];
+        for (int r = tid; r < mc; r += NT) {
+            L.s[r] += alpha * L.ds[r];
+            L.lam[r] += alpha * L.dl[r];
+        }
+        __syncthreads();
+    }
+    if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
+    // ---- active-set polish: proximal method of multipliers on {lam > s}
+    const double idl = 1.0 / P.polDelta, rho = P.polRho;
+    for (int r = tid; r < mc; r += NT) {
+        const bool act = L.lam[r] > L.s[r];
+        L.dd[r] = act ? idl : 0.0;
+        L.la[r] = act ? L.lam[r] : 0.0;   // y
+        L.sa[r] = act ? 1.0 : 0.0;        // active mask
+    }
+    for (int e = tid; e < n; e += NT) L.dz[e] = L.z[e];
+    __syncthreads();
+    assemble<HG>(P, L, L.dd, rho);
+    bool ok = cholesky<HG>(L);
+    if (ok) {
+        for (int ref = 0; ref < P.nRefine; ++ref) {
+            for (int r = tid; r < mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
+            __syncthreads();
+            const double ow = gt_apply(L, L.tv, L.rhs);
+            if (tid == 0) L.rhs[N] = ow - P.slackW + rho * L.dz[N];
+            __syncthreads();
+            for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
+            __syncthreads();
+            chol_solve<HG>(L, L.rhs, L.dz);
+            g_apply(L, L.dz, L.rp, nullptr, true);   // rp = G x - h
+            for (int r = tid; r < mc; r += NT)
+                if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
+            __syncthreads();
+        }
+        double viol = -1e300, ymin = 1e300, ymax = 0.0;
+        for (int r = tid; r < mc; r += NT) {
+            viol = fmax(viol, L.rp[r]);
+            if (L.sa[r] != 0.0) {
+                ymin = fmin(ymin, L.la[r]);
+                ymax = fmax(ymax, fabs(L.la[r]));
+            }
+        }
+        bool fin = true;
+        for (int e = tid; e < n; e += NT) fin = fin && isfinite(L.dz[e]);
+        double red[4] = {viol, -ymin, ymax, fin ? 0.0 : 1.0};
+        block_reduce4(red, 15, L.red);
+        ok = red[0] <= 1e-9 * hmax && -red[1] >= -1e-9 * fmax(1.0, red[2]) && red[3] == 0.0;
+    }
+    if (ok) {
+        for (int e = tid; e < n; e += NT) L.z[e] = L.dz[e];
+    } else {
+        *qflags |= SCPQP_FL_POLISH_REJECTED;
+    }
+    __syncthreads();
+    return it;
+}
+
+// ---------------------------------------------------------------------------
+// Kernel
+// ---------------------------------------------------------------------------
+template <bool HG, bool VG>
+__global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
+    extern __shared__ double smem[];
+    const DevParams& P = *a.P;
+    const int tid = threadIdx.x;
+    double* ws = a.ws ? a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
+    for (;;) {
+        Lay L;
+        carve(&L, smem, ws, P.nV, P.nO, P.hpMax, P.hpMax, HG, VG);
+        int* slot = reinterpret_cast<int*>(L.red + 60);
+        if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
+        __syncthreads();
+        const int b = slot[0];
+        __syncthreads();
+        if (b >= a.B) break;
+        const int Hb = a.hp ? a.hp[b] : P.hpMax;
+        carve(&L, smem, ws, P.nV, P.nO, P.hpMax, Hb, HG, VG);
+        const int V = L.V, N = L.N;
+        const int sflag = setup_problem(a, P, L, b);
+        const int sflag_any = __syncthreads_or(sflag);
+        const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
+        if (a.mode == MODE_SAMPLE) {
+            for (int i = tid; i < Hb * 2 * V; i += NT) {
+                const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
+                a.refOut[(size_t)b * P.hpMax * 2 * V + i] = L.ref[(v * Hb + k) * 2 + c];
+            }
+            continue;
+        }
+        if (a.mode == MODE_LINEARIZE) {
+            for (int i = tid; i < V * Hb * 2; i += NT) {
+                if (a.gOut) a.gOut[slotU * 2 + i] = L.g[i];
+                if (a.p0Out) a.p0Out[slotU * 2 + i] = L.p0[i];
+            }
+            for (int i = tid; i < N; i += NT)
+                if (a.psiOut) a.psiOut[slotU + i] = L.qs[i] / P.uLim;
+            if (a.refOut)
+                for (int i = tid; i < Hb * 2 * V; i += NT) {
+                    const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
+                    a.refOut[(size_t)b * P.hpMax * 2 * V + i] = L.ref[(v * Hb + k) * 2 + c];
+                }
+            __syncthreads();
+            continue;
+        }
+        if (a.mode == MODE_EVALUATE) {
+            for (int i = tid; i < N; i += NT) L.ub[i] = a.uEval[slotU + i];
+            double* cv = a.cveh ? a.cveh + (size_t)b * V * V * P.hpMax : nullptr;
+            double* co = a.cobs ? a.cobs + (size_t)b * V * L.O * P.hpMax : nullptr;
+            if (cv)
+                for (int i = tid; i < V * V * Hb; i += NT) cv[i] = -INFINITY;
+            if (co)
+                for (int i = tid; i < V * L.O * Hb; i += NT) co[i] = -INFINITY;
+            __syncthreads();
+            EvalRes ev = evaluate_u(P, L, L.ub, cv, co);
+            if (tid == 0) {
+                if (a.obj) a.obj[b] = ev.obj;
+                if (a.maxv) a.maxv[b] = ev.maxv;
+                if (a.sumv) a.sumv[b] = ev.sumv;
+                if (a.feas) a.feas[b] = ev.feasible;
+            }
+            if (a.trajOut)
+                for (int i = tid; i < Hb * 2 * V; i += NT) {
+                    const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
+                    a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = L.pb[(v * Hb + k) * 2 + c];
+                }
+            __syncthreads();
+            continue;
+        }
+        // ------------------------------- SCP solve (SCP_controller.py:40-197)
+        for (int i = tid; i < N; i += NT) L.ub[i] = a.uWarm ? a.uWarm[slotU + i] : 0.0;
+        __syncthreads();
+        if (tid == 0 && fabs(L.ub[0]) < 2.220446049250313e-16) L.ub[0] = 2.220446049250313e-16;
+        __syncthreads();
+        EvalRes ev = evaluate_u(P, L, L.ub, nullptr, nullptr);
+        double obj0 = ev.obj, mv0 = ev.maxv;
+        const int maxScp = a.maxScp > 0 ? a.maxScp : P.maxScp;
+        int qflags = 0, nipm = 0, it = 0, status = SCPQP_ST_MAX_SCP;
+        for (it = 0; it < maxScp; ++it) {
+            linearise_rows(P, L);
+            nipm += qp_solve<HG>(P, L, &qflags);
+            for (int i = tid; i < N; i += NT) L.ub[i] = P.uLim * L.z[i];
+            __syncthreads();
+            ev = evaluate_u(P, L, L.ub, nullptr, nullptr);
+            const double delta = (obj0 + P.slackW * mv0) - (ev.obj + P.slackW * ev.maxv);
+            obj0 = ev.obj;
+            mv0 = ev.maxv;
+            if (!isfinite(ev.obj)) {
+                status = SCPQP_ST_NUMERIC;
+                break;
+            }
+            if (V == 1 && fabs(delta) < P.deltaTol && ev.maxv > P.ctol) {
+                status = SCPQP_ST_CONVERGED;
+                break;
+            }
+            if (fabs(delta) < P.deltaTol && ev.maxv <= P.ctol) {
+                status = SCPQP_ST_CONVERGED;
+                break;
+            }
+        }
+        const int nscp = it < maxScp ? it + 1 : maxScp;
+        if (V == 1 && !ev.feasible && status != SCPQP_ST_NUMERIC) status = SCPQP_ST_INVALID;
+        // outputs (positions of the final u are in L.pb from the last evaluate)
+        if (a.uOut)
+            for (int i = tid; i < N; i += NT) a.uOut[slotU + i] = L.ub[i];
+        if (a.trajOut)
+            for (int i = tid; i < Hb * 2 * V; i += NT) {
+                const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
+                a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = L.pb[(v * Hb + k) * 2 + c];
+            }
+        if (tid == 0) {
+            if (a.status) a.status[b] = status | qflags | (sflag_any ? SCPQP_FL_SAMPLER : 0);
+            if (a.nscp) a.nscp[b] = nscp;
+            if (a.nipm) a.nipm[b] = nipm;
+            if (a.obj) a.obj[b] = ev.obj;
+            if (a.maxv) a.maxv[b] = ev.maxv;
+            if (a.sumv) a.sumv[b] = ev.sumv;
+            if (a.feas) a.feas[b] = ev.feasible;
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+thread_local char g_err[512] = "";
+
+int fail(int code, const char* fmt, const char* detail = "") {
+    snprintf(g_err, sizeof(g_err), fmt, detail);
+    return code;
+}
+
+#define HIPCHK(x)                                                               \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) return fail(SCPQP_E_HIP, "HIP error: %s", hipGetErrorString(e_)); \
+    } while (0)
+
+}  // namespace
+
+struct scpqp_handle {
+    scpqp_dims dims;
+    DevParams hostP;
+    DevParams* devP = nullptr;
+    int device = 0;
+    int cus = 256;
+    int* counter = nullptr;
+    double* ws = nullptr;
+    size_t wsBytes = 0;
+    int hG = 0, vG = 0;
+    size_t ldsBytes = 0;
+    long long wsStride = 0;
+    int grid = 0;
+};
+
+namespace {
+
+const size_t kLdsLimit = 163840;
+
+int plan(scpqp_handle* h) {
+    const int V = h->dims.n_veh, O = h->dims.n_obst, Hm = h->dims.hp_max;
+    for (int cfg = 0; cfg < 3; ++cfg) {
+        const bool hG = cfg >= 2, vG = cfg >= 1;
+        Sizes S = carve(nullptr, nullptr, nullptr, V, O, Hm, Hm, hG, vG);
+        const size_t lds = (size_t)(S.persist + S.uni) * sizeof(double);
+        if (lds <= kLdsLimit) {
+            h->hG = hG;
+            h->vG = vG;
+            h->ldsBytes = lds;
+            h->wsStride = S.ws;
+            int perCU = (int)(kLdsLimit / lds);
+            if (perCU > 8) perCU = 8;
+            if (perCU < 1) perCU = 1;
+            h->grid = h->cus * perCU;
+            return 0;
+        }
+    }
+    return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
+}
+
+template <bool HG, bool VG>
+int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
+    auto kern = scp_kernel<HG, VG>;
+    HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->ldsBytes));
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), h->ldsBytes, st, a);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
+    if (a.B <= 0) return 0;
+    HIPCHK(hipSetDevice(h->device));
+    int grid = a.B < h->grid ? a.B : h->grid;
+    if (h->wsStride > 0) {
+        const size_t need = (size_t)grid * h->wsStride * sizeof(double);
+        if (need > h->wsBytes) {
+            if (h->ws) HIPCHK(hipFree(h->ws));
+            h->ws = nullptr;
+            HIPCHK(hipMalloc(&h->ws, need));
+            h->wsBytes = need;
+        }
+    }
+    a.P = h->devP;
+    a.ws = h->ws;
+    a.wsStride = h->wsStride;
+    a.counter = h->counter;
+    HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
+    if (h->hG) return launch_t<true, true>(h, a, st, grid);
+    if (h->vG) return launch_t<false, true>(h, a, st, grid);
+    return launch_t<false, false>(h, a, st, grid);
+}
+
+int check_in(scpqp_handle* h, int32_t B, const scpqp_batch_in* in) {
+    if (!h) return fail(SCPQP_E_ARG, "null handle%s");
+    if (!in || !in->x0) return fail(SCPQP_E_ARG, "null input x0%s");
+    if (B < 0 || B > h->dims.max_batch) return fail(SCPQP_E_ARG, "batch size out of range%s");
+    if (h->dims.n_obst > 0 && !in->obst) return fail(SCPQP_E_ARG, "n_obst > 0 needs obst%s");
+    return 0;
+}
+
+KArgs base_args(int32_t B, const scpqp_batch_in* in) {
+    KArgs a;
+    memset(&a, 0, sizeof(a));
+    a.B = B;
+    a.x0 = in->x0;
+    a.u0 = in->u0;
+    a.ec = in->ec_noise;
+    a.obst = in->obst;
+    a.refIn = in->ref_points;
+    a.uWarm = in->u_warm;
+    a.hp = in->hp;
+    a.maxScp = in->max_scp_iter;
+    return a;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* scpqp_last_error(void) { return g_err; }
+
+const char* scpqp_version(void) { return "scpqp-mi355x 0.1 (gfx950, fp64)"; }
+
+int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpqp_handle** out) {
+    if (!dims || !p || !out) return fail(SCPQP_E_ARG, "null argument%s");
+    *out = nullptr;
+    if (dims->n_veh < 1 || dims->n_veh > SCPQP_MAX_VEH) return fail(SCPQP_E_ARG, "n_veh out of range%s");
+    if (dims->n_obst < 0 || dims->n_obst > SCPQP_MAX_OBST) return fail(SCPQP_E_ARG, "n_obst out of range%s");
+    if (dims->hp_max < 1 || dims->hp_max > SCPQP_MAX_HP) return fail(SCPQP_E_ARG, "hp_max out of range%s");
+    if (dims->n_veh * dims->hp_max + 1 > 256) return fail(SCPQP_E_SIZE, "n_veh*hp_max+1 > 256%s");
+    if (dims->max_batch < 0) return fail(SCPQP_E_ARG, "max_batch < 0%s");
+    if (!p->lf || !p->lr || !p->q || !p->q_final || !p->r || !p->dsafe_veh)
+        return fail(SCPQP_E_ARG, "null per-vehicle parameter%s");
+    if (dims->n_obst > 0 && !p->dsafe_obs) return fail(SCPQP_E_ARG, "n_obst > 0 needs dsafe_obs%s");
+    if (p->ref_max_pts > SCPQP_MAX_REFPTS) return fail(SCPQP_E_ARG, "ref_max_pts too large%s");
+    scpqp_handle* h = new (std::nothrow) scpqp_handle();
+    if (!h) return fail(SCPQP_E_NOMEM, "out of host memory%s");
+    h->dims = *dims;
+    h->device = device;
+    DevParams& P = h->hostP;
+    memset(&P, 0, sizeof(P));
+    const int V = dims->n_veh, O = dims->n_obst;
+    P.nV = V;
+    P.hpMax = dims->hp_max;
+    P.nO = O;
+    P.maxPts = p->ref_max_pts > 0 ? p->ref_max_pts : 2;
+    P.maxScp = p->max_scp_iter > 0 ? p->max_scp_iter : 20;
+    P.maxIpm = p->max_ipm_iter > 0 ? p->max_ipm_iter : 60;
+    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 10;
+    P.flags = p->flags;
+    P.dt = p->dt;
+    P.uLim = p->u_lim;
+    P.ctol = p->constraint_tol;
+    P.deltaTol = p->delta_tol;
+    P.slackW = p->slack_weight;
+    P.ipmTol = p->ipm_tol > 0 ? p->ipm_tol : 1e-9;
+    P.polDelta = p->polish_delta > 0 ? p->polish_delta : 1e-6;
+    P.polRho = p->polish_rho >= 0 ? p->polish_rho : 1e-12;
+    for (int v = 0; v < V; ++v) {
+        P.Lf[v] = p->lf[v];
+        P.Lr[v] = p->lr[v];
+        P.Q[v] = p->q[v];
+        P.Qf[v] = p->q_final[v];
+        P.R[v] = p->r[v];
+        for (int w = 0; w < V; ++w) {
+            const double ds = p->dsafe_veh[v * V + w] + p->dsafe_extra;
+            P.D2veh[v * SCPQP_MAX_VEH + w] = ds * ds;
+        }
+        for (int o = 0; o < O; ++o) {
+            const double ds = p->dsafe_obs[v * O + o] + p->dsafe_extra;
+            P.D2obs[v * SCPQP_MAX_OBST + o] = ds * ds;
+        }
+        const int np = p->ref_npts ? p->ref_npts[v] : 0;
+        P.npts[v] = np;
+        for (int i = 0; i < np && p->ref_polyline; ++i) {
+            P.poly[(v * P.maxPts + i) * 2] = p->ref_polyline[(v * p->ref_max_pts + i) * 2];
+            P.poly[(v * P.maxPts + i) * 2 + 1] = p->ref_polyline[(v * p->ref_max_pts + i) * 2 + 1];
+        }
+    }
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&h->cus, hipDeviceAttributeMultiprocessorCount, device);
+    if (e == hipSuccess) e = hipMalloc(&h->devP, sizeof(DevParams));
+    if (e == hipSuccess) e = hipMemcpy(h->devP, &P, sizeof(DevParams), hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMalloc(&h->counter, sizeof(int));
+    if (e != hipSuccess) {
+        snprintf(g_err, sizeof(g_err), "HIP error: %s", hipGetErrorString(e));
+        scpqp_destroy(h);
+        return SCPQP_E_HIP;
+    }
+    int rc = plan(h);
+    if (rc) {
+        scpqp_destroy(h);
+        return rc;
+    }
+    *out = h;
+    return 0;
+}
+
+int scpqp_destroy(scpqp_handle* h) {
+    if (!h) return 0;
+    (void)hipSetDevice(h->device);
+    if (h->devP) (void)hipFree(h->devP);
+    if (h->counter) (void)hipFree(h->counter);
+    if (h->ws) (void)hipFree(h->ws);
+    delete h;
+    return 0;
+}
+
+int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_batch_out* out,
+                void* stream) {
+    int rc = check_in(h, B, in);
+    if (rc) return rc;
+    if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
+    KArgs a = base_args(B, in);
+    a.mode = MODE_SOLVE;
+    a.uOut = out->u;
+    a.trajOut = out->traj;
+    a.status = out->status;
+    a.nscp = out->n_scp;
+    a.nipm = out->n_ipm;
+    a.obj = out->obj;
+    a.maxv = out->max_violation;
+    a.sumv = out->sum_violations;
+    a.feas = out->feasible;
+    return launch(h, a, static_cast<hipStream_t>(stream));
+}
+
+int scpqp_linearize(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_lin_out* out,
+                    void* stream) {
+    int rc = check_in(h, B, in);
+    if (rc) return rc;
+    if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
+    KArgs a = base_args(B, in);
+    a.mode = MODE_LINEARIZE;
+    a.Ad = out->Ad;
+    a.Bd = out->Bd;
+    a.Ed = out->Ed;
+    a.gOut = out->g;
+    a.p0Out = out->const_term;
+    a.psiOut = out->psi0;
+    a.refOut = out->ref_points;
+    return launch(h, a, static_cast<hipStream_t>(stream));
+}
+
+int scpqp_evaluate(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const double* u,
+                   const scpqp_eval_out* out, void* stream) {
+    int rc = check_in(h, B, in);
+    if (rc) return rc;
+    if (!out || !u) return fail(SCPQP_E_ARG, "null u or output struct%s");
+    KArgs a = base_args(B, in);
+    a.mode = MODE_EVALUATE;
+    a.uEval = u;
+    a.obj = out->obj;
+    a.maxv = out->max_violation;
+    a.sumv = out->sum_violations;
+    a.feas = out->feasible;
+    a.cveh = out->c_veh;
+    a.cobs = out->c_obs;
+    a.trajOut = out->traj;
+    return launch(h, a, static_cast<hipStream_t>(stream));
+}
+
+int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, double* ref,
+                           void* stream) {
+    int rc = check_in(h, B, in);
+    if (rc) return rc;
+    if (!ref) return fail(SCPQP_E_ARG, "null ref_points%s");
+    KArgs a = base_args(B, in);
+    a.refIn = nullptr;
+    a.mode = MODE_SAMPLE;
+    a.refOut = ref;
+    return launch(h, a, static_cast<hipStream_t>(stream));
+}
+
+int scpqp_resources(scpqp_handle* h, int64_t* lds, int64_t* ws, int32_t* big, int32_t* grid) {
+    if (!h) return fail(SCPQP_E_ARG, "null handle%s");
+    if (lds) *lds = (int64_t)h->ldsBytes;
+    if (ws) *ws = (int64_t)h->wsStride * (int64_t)sizeof(double);
+    if (big) *big = h->hG ? 2 : (h->vG ? 1 : 0);
+    if (grid) *grid = h->grid;
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,118 @@
+"""ctypes binding of ``include/scpqp.h`` (the C-ABI of the HIP library).
+
+The shared library ``libscpqp.so`` is built in-tree (``__graft_entry__.build()``
+or ``python -m scpqp.build``).  There is no CPU fallback: if the library or a
+GPU is missing, loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libscpqp.so")
+
+MAX_VEH = 16
+MAX_OBST = 32
+MAX_REFPTS = 8
+MAX_HP = 64
+
+ST_CONVERGED = 0
+ST_MAX_SCP = 1
+ST_INVALID = 2
+ST_NUMERIC = 3
+FL_POLISH_REJECTED = 0x100
+FL_IPM_MAXIT = 0x200
+FL_SAMPLER = 0x400
+FLAG_OBST_QUIRK = 1
+
+_dp = C.POINTER(C.c_double)
+_ip = C.POINTER(C.c_int32)
+
+
+class Dims(C.Structure):
+    _fields_ = [("n_veh", C.c_int32), ("hp_max", C.c_int32), ("n_obst", C.c_int32),
+                ("max_batch", C.c_int32)]
+
+
+class Params(C.Structure):
+    _fields_ = [("dt", C.c_double), ("u_lim", C.c_double), ("dsafe_extra", C.c_double),
+                ("constraint_tol", C.c_double), ("delta_tol", C.c_double),
+                ("slack_weight", C.c_double), ("max_scp_iter", C.c_int32),
+                ("max_ipm_iter", C.c_int32), ("polish_refine", C.c_int32), ("flags", C.c_int32),
+                ("ipm_tol", C.c_double), ("polish_delta", C.c_double), ("polish_rho", C.c_double),
+                ("lf", _dp), ("lr", _dp), ("q", _dp), ("q_final", _dp), ("r", _dp),
+                ("dsafe_veh", _dp), ("dsafe_obs", _dp), ("ref_polyline", _dp),
+                ("ref_npts", _ip), ("ref_max_pts", C.c_int32)]
+
+
+class BatchIn(C.Structure):
+    _fields_ = [("x0", C.c_void_p), ("u0", C.c_void_p), ("ec_noise", C.c_void_p),
+                ("hp", C.c_void_p), ("obst", C.c_void_p), ("ref_points", C.c_void_p),
+                ("u_warm", C.c_void_p), ("max_scp_iter", C.c_int32), ("reserved", C.c_int32)]
+
+
+class BatchOut(C.Structure):
+    _fields_ = [("u", C.c_void_p), ("traj", C.c_void_p), ("status", C.c_void_p),
+                ("n_scp", C.c_void_p), ("n_ipm", C.c_void_p), ("obj", C.c_void_p),
+                ("max_violation", C.c_void_p), ("sum_violations", C.c_void_p),
+                ("feasible", C.c_void_p)]
+
+
+class LinOut(C.Structure):
+    _fields_ = [("Ad", C.c_void_p), ("Bd", C.c_void_p), ("Ed", C.c_void_p), ("g", C.c_void_p),
+                ("const_term", C.c_void_p), ("psi0", C.c_void_p), ("ref_points", C.c_void_p)]
+
+
+class EvalOut(C.Structure):
+    _fields_ = [("obj", C.c_void_p), ("max_violation", C.c_void_p),
+                ("sum_violations", C.c_void_p), ("feasible", C.c_void_p), ("c_veh", C.c_void_p),
+                ("c_obs", C.c_void_p), ("traj", C.c_void_p)]
+
+
+# every symbol include/scpqp.h declares (checked by tests/test_abi.py)
+EXPORTS = ("scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version", "scpqp_solve",
+           "scpqp_linearize", "scpqp_evaluate", "scpqp_sample_reference", "scpqp_resources")
+
+_lib = None
+
+
+def load(path=None):
+    """Load the HIP library (raises OSError if it was not built)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise OSError(f"scpqp: HIP library not built ({p}); run __graft_entry__.build()")
+    lib = C.CDLL(p)
+    H = C.c_void_p
+    lib.scpqp_create.argtypes = [C.POINTER(Dims), C.POINTER(Params), C.c_int, C.POINTER(H)]
+    lib.scpqp_create.restype = C.c_int
+    lib.scpqp_destroy.argtypes = [H]
+    lib.scpqp_destroy.restype = C.c_int
+    lib.scpqp_last_error.argtypes = []
+    lib.scpqp_last_error.restype = C.c_char_p
+    lib.scpqp_version.argtypes = []
+    lib.scpqp_version.restype = C.c_char_p
+    lib.scpqp_solve.argtypes = [H, C.c_int32, C.POINTER(BatchIn), C.POINTER(BatchOut), C.c_void_p]
+    lib.scpqp_solve.restype = C.c_int
+    lib.scpqp_linearize.argtypes = [H, C.c_int32, C.POINTER(BatchIn), C.POINTER(LinOut), C.c_void_p]
+    lib.scpqp_linearize.restype = C.c_int
+    lib.scpqp_evaluate.argtypes = [H, C.c_int32, C.POINTER(BatchIn), C.c_void_p,
+                                   C.POINTER(EvalOut), C.c_void_p]
+    lib.scpqp_evaluate.restype = C.c_int
+    lib.scpqp_sample_reference.argtypes = [H, C.c_int32, C.POINTER(BatchIn), C.c_void_p, C.c_void_p]
+    lib.scpqp_sample_reference.restype = C.c_int
+    lib.scpqp_resources.argtypes = [H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
+                                    C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.scpqp_resources.restype = C.c_int
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(rc, lib=None):
+    if rc != 0:
+        lib = lib or load()
+        raise RuntimeError(f"scpqp error {rc}: {lib.scpqp_last_error().decode()}")
