@@ -15,8 +15,10 @@
 // early (fewer SCP iterations, shorter horizon) immediately take the next one.
 // Everything is fp64.  The per-problem state (KKT matrix, Toeplitz blocks,
 // interior-point vectors) lives in LDS; when it does not fit (8 vehicles at
-// Hp=30), the KKT matrix and/or the constraint vectors move to a per-workgroup
-// global workspace (template flags H_G / V_G).
+// Hp=30, or 4 vehicles at Hp=30), the KKT matrix and/or the constraint vectors
+// move to a per-workgroup global workspace (template flags HG / VG).  All LDS
+// arrays are addressed through address_space(3) pointers so every access is a
+// ds_read/ds_write, never a flat access.
 //
 // The QP is solved in scaled variables (controls in units of
 // uLim, every constraint row of unit norm) by a Mehrotra predictor-corrector
@@ -38,6 +40,7 @@
 #include <string.h>
 
 #include <new>
+#include <type_traits>
 
 #include "scpqp.h"
 
@@ -46,6 +49,32 @@
 #define SCR_PER_WAVE 640
 
 namespace {
+
+// Diagnostic phase stamps (built only with -DSCPQP_PROF; never in the shipped kernel).
+#ifdef SCPQP_PROF
+__device__ unsigned long long g_prof[16];
+#define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
+#define PROF_ACC(cat)                                                              \
+    do {                                                                           \
+        unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
+        if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&g_prof[cat], _t1 - _pt); \
+        _pt = _t1;                                                                 \
+    } while (0)
+#else
+#define PROF_T0() (void)0
+#define PROF_ACC(cat) (void)0
+#endif
+
+typedef __attribute__((address_space(3))) double ldouble;
+typedef __attribute__((address_space(3))) int lint;
+typedef __attribute__((address_space(1))) double gdouble;
+typedef double double2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) double2v ldouble2;
+typedef __attribute__((address_space(1))) double2v gdouble2;
+
+// 16-byte loads (ds_read_b128 / global_load_dwordx4); callers pass even offsets
+__device__ __forceinline__ double2v ld2(const ldouble* p) { return *(const ldouble2*)p; }
+__device__ __forceinline__ double2v ld2(const gdouble* p) { return *(const gdouble2*)p; }
 
 // ---------------------------------------------------------------------------
 // Parameters (device copy of scpqp_params with derived constants)
@@ -79,95 +108,103 @@ struct KArgs {
 };
 
 // ---------------------------------------------------------------------------
-// Per-problem layout.  Sizes allocate for hp_max; indexing uses the problem's
-// own horizon Hb, so a mixed-horizon batch shares one launch.
+// Memory plan: integer offsets (doubles).  Persistent LDS arrays first, then a
+// union region used by the setup scratch (expm) and, during the solve, by the
+// KKT matrix, the W~ blocks and the 9 constraint-space vectors (those marked
+// global go to the per-workgroup workspace instead).  Sizes use hp_max;
+// indexing uses the problem's own horizon, so mixed horizons share a launch.
 // ---------------------------------------------------------------------------
-struct Lay {
-    int V, O, Hb, N, n, m, mc, ld, mp, nb;
-    double *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
-    double *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr;
-    int* rinfo;
-    double *H, *Wt;
-    double *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
-};
-
 __host__ __device__ inline int pad2(int x) { return (x + 1) & ~1; }
 
-struct Sizes {
-    int persist, uni, ws;   // doubles
+struct Off {
+    int x0, u0, ec, g, p0, ref, ob, ub, pb, ya, yb, qs, rowE, rowW, rowH, rinfo;
+    int z, dz, rhs, rd, dinv, red, scr;
+    int H, Wt, vec;     // H and vec in LDS (after persist) or workspace, see hG / vG
+    int persist, uni, ws;
+    int ldAlloc, mcAlloc;
 };
 
-// Carve the layout; with null bases only sizes are computed (host planning).
-__host__ __device__ inline Sizes carve(Lay* L, double* lds, double* ws, int V, int O, int Hm,
-                                       int Hb, bool hG, bool vG) {
+__host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool vG) {
     const int N = V * Hm, n = N + 1, m = V * (V - 1) / 2 * Hm + V * O * Hm;
-    const int mc = m + 2 * N + 1, ld = n | 1, nb = V * (V + 1) / 2;
+    const int mc = m + 2 * N + 1, ld = n + ((6 - n % 4) % 4), nb = V * (V + 1) / 2;
+    Off f;
     int p = 0;
-    auto take = [&](double** dst, int cnt) {
-        if (lds && dst) *dst = lds + p;
-        p += pad2(cnt);
-    };
-    take(L ? &L->x0 : nullptr, 6 * V);
-    take(L ? &L->u0 : nullptr, V);
-    take(L ? &L->ec : nullptr, 2 * V);
-    take(L ? &L->g : nullptr, 2 * V * Hm);
-    take(L ? &L->p0 : nullptr, 2 * V * Hm);
-    take(L ? &L->ref : nullptr, 2 * V * Hm);
-    take(L ? &L->ob : nullptr, 2 * O * Hm);
-    take(L ? &L->ub : nullptr, V * Hm);
-    take(L ? &L->pb : nullptr, 2 * V * Hm);
-    take(L ? &L->ya : nullptr, 2 * V * Hm);
-    take(L ? &L->yb : nullptr, 2 * V * Hm);
-    take(L ? &L->qs : nullptr, V * Hm);
-    take(L ? &L->rowE : nullptr, 2 * m);
-    take(L ? &L->rowW : nullptr, m);
-    take(L ? &L->rowH : nullptr, m);
-    {
-        double* ri = nullptr;
-        take(&ri, (m + 1) / 2);
-        if (L && lds) L->rinfo = reinterpret_cast<int*>(ri);
-    }
-    take(L ? &L->z : nullptr, n);
-    take(L ? &L->dz : nullptr, n);
-    take(L ? &L->rhs : nullptr, n);
-    take(L ? &L->rd : nullptr, n);
-    take(L ? &L->dinv : nullptr, n);
-    take(L ? &L->red : nullptr, 64);
-    Sizes S;
-    S.persist = p;
-    // union region: setup scratch  |  solve arrays
-    const int setup = NWAVE * SCR_PER_WAVE;
+    f.x0 = p; p += pad2(6 * V);
+    f.u0 = p; p += pad2(V);
+    f.ec = p; p += pad2(2 * V);
+    f.g = p; p += pad2(2 * N);
+    f.p0 = p; p += pad2(2 * N);
+    f.ref = p; p += pad2(2 * N);
+    f.ob = p; p += pad2(2 * O * Hm);
+    f.ub = p; p += pad2(N);
+    f.pb = p; p += pad2(2 * N);
+    f.ya = p; p += pad2(2 * N);
+    f.yb = p; p += pad2(2 * N);
+    f.qs = p; p += pad2(N);
+    f.rowE = p; p += pad2(2 * m);
+    f.rowW = p; p += pad2(m);
+    f.rowH = p; p += pad2(m);
+    f.rinfo = p; p += pad2((m + 1) / 2);
+    f.z = p; p += pad2(n);
+    f.dz = p; p += pad2(n);
+    f.rhs = p; p += pad2(n);
+    f.rd = p; p += pad2(n);
+    f.dinv = p; p += pad2(n);
+    f.red = p; p += 64;
+    f.persist = p;
+    f.scr = p;
     int u = 0, w = 0;
-    auto takeU = [&](double** dst, int cnt, bool global) {
-        if (global) {
-            if (ws && dst) *dst = ws + w;
-            w += pad2(cnt);
-        } else {
-            if (lds && dst) *dst = lds + p + u;
-            u += pad2(cnt);
-        }
-    };
-    takeU(L ? &L->H : nullptr, n * ld, hG);
-    takeU(L ? &L->Wt : nullptr, 4 * Hm * nb, false);
-    double** vec[9] = {nullptr};
-    if (L) {
-        vec[0] = &L->s; vec[1] = &L->lam; vec[2] = &L->ds; vec[3] = &L->dl; vec[4] = &L->rp;
-        vec[5] = &L->dd; vec[6] = &L->sa; vec[7] = &L->la; vec[8] = &L->tv;
-    }
-    for (int i = 0; i < 9; ++i) takeU(vec[i], mc, vG);
-    if (L && lds) L->scr = lds + p;
-    S.uni = u > setup ? u : setup;
-    S.ws = w;
-    if (L) {
-        L->V = V; L->O = O; L->Hb = Hb; L->N = V * Hb; L->n = L->N + 1;
-        L->mp = V * (V - 1) / 2 * Hb;
-        L->m = L->mp + V * O * Hb;
-        L->mc = L->m + 2 * L->N + 1;
-        L->ld = ld;           // allocation leading dimension (odd: conflict-free columns)
-        L->nb = nb;
-    }
-    return S;
+    if (hG) { f.H = w; w += pad2(n * ld); } else { f.H = p + u; u += pad2(n * ld); }
+    f.Wt = p + u; u += pad2(4 * Hm * nb);
+    if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
+    const int setup = NWAVE * SCR_PER_WAVE;
+    f.uni = u > setup ? u : setup;
+    f.ws = w;
+    f.ldAlloc = ld;
+    f.mcAlloc = pad2(mc);
+    return f;
 }
+
+template <bool HG, bool VG, int RM>
+struct Lay {
+    static constexpr int RMAX = RM;   // row slots of the triangular solves (n <= 64 RM)
+    using HT = typename std::conditional<HG, gdouble, ldouble>::type;
+    using VT = typename std::conditional<VG, gdouble, ldouble>::type;
+    int V, O, Hb, N, n, m, mc, ld, mp, nb;
+    ldouble *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
+    ldouble *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr, *Wt;
+    lint* rinfo;
+    HT* H;
+    VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
+};
+
+template <bool HG, bool VG, int RM>
+__device__ __forceinline__ Lay<HG, VG, RM> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
+                                                    int O, int Hb) {
+    Lay<HG, VG, RM> L;
+    L.V = V; L.O = O; L.Hb = Hb; L.N = V * Hb; L.n = L.N + 1;
+    L.mp = V * (V - 1) / 2 * Hb;
+    L.m = L.mp + V * O * Hb;
+    L.mc = L.m + 2 * L.N + 1;
+    L.ld = f.ldAlloc;
+    L.nb = V * (V + 1) / 2;
+    L.x0 = lds + f.x0; L.u0 = lds + f.u0; L.ec = lds + f.ec; L.g = lds + f.g; L.p0 = lds + f.p0;
+    L.ref = lds + f.ref; L.ob = lds + f.ob; L.ub = lds + f.ub; L.pb = lds + f.pb;
+    L.ya = lds + f.ya; L.yb = lds + f.yb; L.qs = lds + f.qs; L.rowE = lds + f.rowE;
+    L.rowW = lds + f.rowW; L.rowH = lds + f.rowH; L.z = lds + f.z; L.dz = lds + f.dz;
+    L.rhs = lds + f.rhs; L.rd = lds + f.rd; L.dinv = lds + f.dinv; L.red = lds + f.red;
+    L.scr = lds + f.scr; L.Wt = lds + f.Wt;
+    L.rinfo = (lint*)(lds + f.rinfo);
+    if constexpr (HG) L.H = ws + f.H; else L.H = lds + f.H;
+    typename Lay<HG, VG, RM>::VT* vb;
+    if constexpr (VG) vb = ws + f.vec; else vb = lds + f.vec;
+    const int st = f.mcAlloc;
+    L.s = vb; L.lam = vb + st; L.ds = vb + 2 * st; L.dl = vb + 3 * st; L.rp = vb + 4 * st;
+    L.dd = vb + 5 * st; L.sa = vb + 6 * st; L.la = vb + 7 * st; L.tv = vb + 8 * st;
+    return L;
+}
+
+extern __shared__ double smem_[];   // dynamic LDS (one problem's state)
 
 // ---------------------------------------------------------------------------
 // Small helpers
@@ -190,15 +227,9 @@ __device__ __forceinline__ double wave_max(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
     return v;
 }
-__device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-    return v;
-}
 
-// Reduce four values across the workgroup; ops: bit q set = max, else sum.
-// (min is expressed as max of negated values by callers.)
-__device__ __forceinline__ void block_reduce4(double* v, int maxmask, double* red) {
+// Reduce four values across the workgroup; bit q of maxmask: max, else sum.
+__device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldouble* red) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = (maxmask >> q & 1) ? wave_max(v[q]) : wave_sum(v[q]);
@@ -224,23 +255,25 @@ __device__ __forceinline__ int pair_index(int i, int j, int V) {
 
 // Row r -> (i, j, o, k): vehicle pair rows (i<j, k innermost) then obstacle
 // rows (v, o, k) — the order of SCP_controller.py:97-114.
-__device__ __forceinline__ void row_decode(const Lay& L, int info, int& i, int& j, int& o,
-                                           int& k) {
+__device__ __forceinline__ void row_decode(int info, int& i, int& j, int& o, int& k) {
     i = info & 0xff;
     j = ((info >> 8) & 0xff) - 1;
     o = ((info >> 16) & 0xff) - 1;
     k = (info >> 24) & 0xff;
 }
 
-__device__ __forceinline__ double hval(const Lay& L, int i) {
+template <class LT>
+__device__ __forceinline__ double hval(const LT& L, int i) {
     return i < L.m ? L.rowH[i] : (i < L.mc - 1 ? 1.0 : 0.0);
 }
 
 // ---------------------------------------------------------------------------
-// Vehicle model (Model.py:45-87)
+// Vehicle model (Model.py:45-87): entry (i, j) of the 8x8 expm argument
+// [[Ac Bc Ec]; 0] computed per lane.
 // ---------------------------------------------------------------------------
-__device__ void bicycle_jacobian(const double* x, double u, double Lf, double Lr, double n0,
-                                 double n1, double Ac[6][6], double Ec[6]) {
+__device__ double jac_entry(const ldouble* x, double u, double Lf, double Lr, double n0, double n1,
+                            int i, int j) {
+    if (i >= 6) return 0.0;
     const double L = Lf + Lr, rho = Lr / L;
     const double v = x[3], psi = x[2], d = x[5];
     const double t = tan(d), sec2 = t * t + 1.0;
@@ -248,36 +281,29 @@ __device__ void bicycle_jacobian(const double* x, double u, double Lf, double Lr
     const double beta = atan(rho * t);
     const double th = psi + beta;
     const double cth = cos(th), sth = sin(th);
-#pragma unroll
-    for (int i = 0; i < 6; ++i)
-#pragma unroll
-        for (int j = 0; j < 6; ++j) Ac[i][j] = 0.0;
-    Ac[0][2] = -v * sth * kap;
-    Ac[0][3] = cth * kap;
-    Ac[0][5] = rho * rho * v * cth * t * sec2 / kap - rho * v * sth * sec2 / kap;
-    Ac[1][2] = v * cth * kap;
-    Ac[1][3] = sth * kap;
-    Ac[1][5] = rho * v * cth * sec2 / kap + rho * rho * v * sth * t * sec2 / kap;
-    Ac[2][3] = t / L;
-    Ac[2][5] = v * sec2 / L;
-    Ac[3][4] = 1.0;
-    Ac[5][5] = -10.0;
-    // f(x, u) (Model.py:69-87) with the two noise draws on dx[0], dx[1]
-    const double vc = v * sqrt(1.0 + (rho * t) * (rho * t));
-    double f[6];
-    f[0] = vc * cos(psi + beta) + n0;
-    f[1] = vc * sin(psi + beta) + n1;
-    f[2] = vc * t * cos(beta) / L;
-    f[3] = x[4];
-    f[4] = 0.0;
-    f[5] = (u - x[5]) / 0.1;
-#pragma unroll
-    for (int i = 0; i < 6; ++i) {
-        double ax = 0.0;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) ax += Ac[i][j] * x[j];
-        Ec[i] = f[i] - ax - (i == 5 ? 10.0 * u : 0.0);
+    // analytic Ac (Model.py:46-52)
+    double a02 = -v * sth * kap, a03 = cth * kap;
+    double a05 = rho * rho * v * cth * t * sec2 / kap - rho * v * sth * sec2 / kap;
+    double a12 = v * cth * kap, a13 = sth * kap;
+    double a15 = rho * v * cth * sec2 / kap + rho * rho * v * sth * t * sec2 / kap;
+    double a23 = t / L, a25 = v * sec2 / L;
+    if (j < 6) {
+        if (i == 0) return j == 2 ? a02 : j == 3 ? a03 : j == 5 ? a05 : 0.0;
+        if (i == 1) return j == 2 ? a12 : j == 3 ? a13 : j == 5 ? a15 : 0.0;
+        if (i == 2) return j == 3 ? a23 : j == 5 ? a25 : 0.0;
+        if (i == 3) return j == 4 ? 1.0 : 0.0;
+        if (i == 5) return j == 5 ? -10.0 : 0.0;
+        return 0.0;
     }
+    if (j == 6) return i == 5 ? 10.0 : 0.0;   // Bc (Model.py:53)
+    // Ec = f(x,u) - Ac x - Bc u   (Model.py:58), noise on dx[0], dx[1] (:84-86)
+    const double vc = v * sqrt(1.0 + (rho * t) * (rho * t));
+    if (i == 0) return (vc * cos(psi + beta) + n0) - (a02 * x[2] + a03 * x[3] + a05 * x[5]);
+    if (i == 1) return (vc * sin(psi + beta) + n1) - (a12 * x[2] + a13 * x[3] + a15 * x[5]);
+    if (i == 2) return vc * t * cos(beta) / L - (a23 * x[3] + a25 * x[5]);
+    if (i == 3) return x[4] - x[4];
+    if (i == 4) return 0.0;
+    return (u - x[5]) / 0.1 - (-10.0 * x[5]) - 10.0 * u;
 }
 
 // ---------------------------------------------------------------------------
@@ -286,7 +312,7 @@ __device__ void bicycle_jacobian(const double* x, double u, double Lf, double Lr
 // B.2's float '^' (reference raises) is evaluated with '**' and flagged.
 // ---------------------------------------------------------------------------
 __device__ int sample_reference(const DevParams& P, int v, double vx, double vy, double step,
-                                int Hb, double* out /* [Hb][2] */) {
+                                int Hb, ldouble* out /* [Hb][2] */) {
     const double* c = P.poly + v * P.maxPts * 2;
     const int np = P.npts[v];
     int flag = 0;
@@ -363,32 +389,29 @@ __device__ int sample_reference(const DevParams& P, int v, double vx, double vy,
 // expm(dt [[Ac Bc Ec];0]) gives Ad, Bd and Ed at once.
 // All waves execute the same barrier sequence (`act` masks the work).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ double mm_entry(const double* A, const double* B, int i, int j) {
+__device__ __forceinline__ double mm_entry(const ldouble* A, const ldouble* B, int i, int j) {
     double acc = 0.0;
 #pragma unroll
     for (int k = 0; k < 8; ++k) acc += A[i * 8 + k] * B[k * 8 + j];
     return acc;
 }
 
-__device__ void expm8(double* scr, bool act, double* red) {
-    // scr: M(0) A(64) A2(128) A4(192) A6(256) T1(320) T2(384) U(448) Vv(512) aug(0..127 reuse M,A)
+__device__ void expm8(ldouble* scr, bool act, ldouble* red) {
     const int lane = threadIdx.x & 63, i = lane >> 3, j = lane & 7;
-    double* M = scr;
-    double* A = scr + 64;
-    double* A2 = scr + 128;
-    double* A4 = scr + 192;
-    double* A6 = scr + 256;
-    double* T1 = scr + 320;
-    double* T2 = scr + 384;
-    double* U = scr + 448;
-    double* Vv = scr + 512;
-    const double b[14] = {64764752532480000.0, 32382376266240000.0, 7771770303897600.0,
-                          1187353796428800.0,  129060195264000.0,   10559470521600.0,
-                          670442572800.0,      33522128640.0,       1323241920.0,
-                          40840800.0,          960960.0,            16380.0,
-                          182.0,               1.0};
+    ldouble* M = scr;
+    ldouble* A = scr + 64;
+    ldouble* A2 = scr + 128;
+    ldouble* A4 = scr + 192;
+    ldouble* A6 = scr + 256;
+    ldouble* T1 = scr + 320;
+    ldouble* T2 = scr + 384;
+    ldouble* U = scr + 448;
+    ldouble* Vv = scr + 512;
+    const double b0 = 64764752532480000.0, b1 = 32382376266240000.0, b2 = 7771770303897600.0,
+                 b3 = 1187353796428800.0, b4 = 129060195264000.0, b5 = 10559470521600.0,
+                 b6 = 670442572800.0, b7 = 33522128640.0, b8 = 1323241920.0, b9 = 40840800.0,
+                 b10 = 960960.0, b11 = 16380.0, b12 = 182.0, b13 = 1.0;
     const double theta13 = 5.371920351148152;
-    // 1-norm and scaling exponent
     double cs = 0.0;
     if (act) {
 #pragma unroll
@@ -411,38 +434,35 @@ __device__ void expm8(double* scr, bool act, double* red) {
     if (act) A6[lane] = mm_entry(A4, A2, i, j);
     __syncthreads();
     if (act) {
-        T1[lane] = b[13] * A6[lane] + b[11] * A4[lane] + b[9] * A2[lane];
-        T2[lane] = b[12] * A6[lane] + b[10] * A4[lane] + b[8] * A2[lane];
+        T1[lane] = b13 * A6[lane] + b11 * A4[lane] + b9 * A2[lane];
+        T2[lane] = b12 * A6[lane] + b10 * A4[lane] + b8 * A2[lane];
     }
     __syncthreads();
     const double id = (i == j) ? 1.0 : 0.0;
     if (act) {
-        U[lane] = mm_entry(A6, T1, i, j) + b[7] * A6[lane] + b[5] * A4[lane] + b[3] * A2[lane] +
-                  b[1] * id;
-        Vv[lane] = mm_entry(A6, T2, i, j) + b[6] * A6[lane] + b[4] * A4[lane] + b[2] * A2[lane] +
-                   b[0] * id;
+        U[lane] = mm_entry(A6, T1, i, j) + b7 * A6[lane] + b5 * A4[lane] + b3 * A2[lane] + b1 * id;
+        Vv[lane] = mm_entry(A6, T2, i, j) + b6 * A6[lane] + b4 * A4[lane] + b2 * A2[lane] + b0 * id;
     }
     __syncthreads();
     if (act) T1[lane] = mm_entry(A, U, i, j);   // U = A * U2
     __syncthreads();
     // augmented [V-U | V+U] (8 x 16) in aug = scr[0..127]
-    double* aug = scr;
+    ldouble* aug = scr;
     if (act) {
         aug[i * 16 + j] = Vv[lane] - T1[lane];
         aug[i * 16 + 8 + j] = Vv[lane] + T1[lane];
     }
     __syncthreads();
-    // Gauss-Jordan with partial pivoting
+    // Gauss-Jordan with partial pivoting (first maximal pivot, as LAPACK idamax)
     for (int k = 0; k < 8; ++k) {
         double key = -1.0;
         if (act && lane < 8 && lane >= k) key = fabs(aug[lane * 16 + k]);
-        // argmax over lanes: pack (key, lane) by comparing
-        double best = wave_max(key);
+        const double best = wave_max(key);
         unsigned long long ball = __ballot(act && lane < 8 && lane >= k && key == best);
-        int p = ball ? __ffsll((long long)ball) - 1 : k;
+        const int p = ball ? __ffsll((long long)ball) - 1 : k;
         __syncthreads();
         if (act && p != k && lane < 16) {
-            double t0 = aug[k * 16 + lane];
+            const double t0 = aug[k * 16 + lane];
             aug[k * 16 + lane] = aug[p * 16 + lane];
             aug[p * 16 + lane] = t0;
         }
@@ -451,15 +471,13 @@ __device__ void expm8(double* scr, bool act, double* red) {
         if (act) {
             const double piv = aug[k * 16 + k];
             const double fi = aug[i * 16 + k];
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const int c = j + 8 * h;
-                double val = aug[i * 16 + c];
-                if (i == k)
-                    val = val / piv;
-                else
-                    val = val - fi * (aug[k * 16 + c] / piv);
-                if (h == 0) nv0 = val; else nv1 = val;
+            const double a0 = aug[i * 16 + j], a1 = aug[i * 16 + 8 + j];
+            if (i == k) {
+                nv0 = a0 / piv;
+                nv1 = a1 / piv;
+            } else {
+                nv0 = a0 - fi * (aug[k * 16 + j] / piv);
+                nv1 = a1 - fi * (aug[k * 16 + 8 + j] / piv);
             }
         }
         __syncthreads();
@@ -478,7 +496,7 @@ __device__ void expm8(double* scr, bool act, double* red) {
     }
     for (int q = 0; q < smax; ++q) {
         const bool sq = act && q < s;
-        double v = sq ? mm_entry(A, A, i, j) : 0.0;
+        const double v = sq ? mm_entry(A, A, i, j) : 0.0;
         __syncthreads();
         if (sq) A[lane] = v;
         __syncthreads();
@@ -489,9 +507,9 @@ __device__ void expm8(double* scr, bool act, double* red) {
 // ---------------------------------------------------------------------------
 // Problem setup: inputs, reference sampling, per-vehicle linearisation
 // (MPCclass, MPC_Iter.py:59-149), scaled cost gradient, row table.
-// Returns sampler flag.
 // ---------------------------------------------------------------------------
-__device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) {
+template <class LT>
+__device__ int setup_problem(const KArgs& a, const DevParams& P, const LT& L, int b) {
     const int tid = threadIdx.x, V = L.V, O = L.O, Hb = L.Hb, Hm = P.hpMax;
     for (int i = tid; i < 6 * V; i += NT) L.x0[i] = a.x0[(size_t)b * V * 6 + i];
     for (int i = tid; i < V; i += NT) L.u0[i] = a.u0 ? a.u0[(size_t)b * V + i] : 0.0;
@@ -508,7 +526,7 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) 
             L.ref[(v * Hb + k) * 2 + c] = a.refIn[(size_t)b * Hm * 2 * V + i];
         }
     } else if (tid < V) {
-        const double* xv = L.x0 + 6 * tid;
+        const ldouble* xv = L.x0 + 6 * tid;
         sflag = sample_reference(P, tid, xv[0], xv[1], xv[3] * P.dt, Hb, L.ref + tid * Hb * 2);
     }
     __syncthreads();
@@ -519,38 +537,20 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) 
     for (int r0 = 0; r0 < V; r0 += NWAVE) {
         const int v = r0 + w;
         const bool act = v < V;
-        double* scr = L.scr + w * SCR_PER_WAVE;
+        ldouble* scr = L.scr + w * SCR_PER_WAVE;
         if (act) {
-            double Ac[6][6], Ec[6];
-            bicycle_jacobian(L.x0 + 6 * v, L.u0[v], P.Lf[v], P.Lr[v], L.ec[2 * v], L.ec[2 * v + 1],
-                             Ac, Ec);
-            const int i = lane >> 3, j = lane & 7;
-            double mv = 0.0;
-            if (i < 6) {
-                if (j < 6) {
-                    // static indexing into Ac via unrolled select
-#pragma unroll
-                    for (int ii = 0; ii < 6; ++ii)
-#pragma unroll
-                        for (int jj = 0; jj < 6; ++jj)
-                            if (ii == i && jj == j) mv = Ac[ii][jj];
-                } else if (j == 6) {
-                    mv = (i == 5) ? 10.0 : 0.0;
-                } else {
-#pragma unroll
-                    for (int ii = 0; ii < 6; ++ii)
-                        if (ii == i) mv = Ec[ii];
-                }
-            }
-            scr[lane] = P.dt * mv;
+            scr[lane] = P.dt * jac_entry(L.x0 + 6 * v, L.u0[v], P.Lf[v], P.Lr[v], L.ec[2 * v],
+                                         L.ec[2 * v + 1], lane >> 3, lane & 7);
         }
         __syncthreads();
         expm8(scr, act, L.red);
         // Ad = X[0:6,0:6], Bd = X[0:6,6], Ed = X[0:6,7] (threshold 1e-30, MPC_Iter.py:87)
         double adrow[6];
         double bi = 0.0, ei = 0.0, xi = 0.0;
-        const double* X = scr + 64;
-        const int comp = lane < 8 ? lane : lane - 8;   // lanes 0..5: state recursion, 8..13: impulse
+        const ldouble* X = scr + 64;
+        const int comp = lane < 8 ? lane : lane - 8;   // lanes 0..5: state, 8..13: impulse
+#pragma unroll
+        for (int jj = 0; jj < 6; ++jj) adrow[jj] = 0.0;
         if (act && comp < 6 && lane < 16) {
 #pragma unroll
             for (int jj = 0; jj < 6; ++jj) adrow[jj] = X[comp * 8 + jj];
@@ -558,28 +558,25 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) 
             ei = X[comp * 8 + 7];
             if (fabs(ei) <= 1e-30) ei = 0.0;
             xi = L.x0[6 * v + comp];
-        } else {
-#pragma unroll
-            for (int jj = 0; jj < 6; ++jj) adrow[jj] = 0.0;
         }
         if (act && a.mode == MODE_LINEARIZE && lane < 6) {
             const size_t base = ((size_t)b * V + v);
             if (a.Ad)
+#pragma unroll
                 for (int jj = 0; jj < 6; ++jj) a.Ad[base * 36 + lane * 6 + jj] = adrow[jj];
             if (a.Bd) a.Bd[base * 6 + lane] = bi;
             if (a.Ed) a.Ed[base * 6 + lane] = ei;
         }
-        // recursions: x_{k+1} = Ad x_k + Ed  (p0_k = C x_{k+1});  b_{m+1} = Ad b_m (g_m = C b_m)
+        // recursions: x_{k+1} = Ad x_k + Ed (p0_k = C x_{k+1});  b_{m+1} = Ad b_m (g_m = C b_m)
         double cur = (lane < 8) ? xi : bi;
         const double add = (lane < 8) ? ei : 0.0;
         const int base = lane < 8 ? 0 : 8;
         for (int k = 0; k < Hb; ++k) {
-            if (lane >= 8 && lane < 14 && act && comp < 2) L.g[(v * Hb + k) * 2 + comp] = cur;
+            if (lane >= 8 && lane < 10 && act) L.g[(v * Hb + k) * 2 + comp] = cur;
             double nxt = add;
 #pragma unroll
             for (int jj = 0; jj < 6; ++jj) nxt += adrow[jj] * __shfl(cur, base + jj, 64);
-            if (lane < 8) cur = nxt;
-            if (lane >= 8) cur = nxt;
+            cur = nxt;
             if (lane < 2 && act) L.p0[(v * Hb + k) * 2 + lane] = cur;
         }
         __syncthreads();
@@ -590,7 +587,7 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) 
         double acc = 0.0;
         for (int k = l; k < Hb; ++k) {
             const double qk = (k == Hb - 1) ? P.Qf[v] : P.Q[v];
-            const double* gg = L.g + (v * Hb + k - l) * 2;
+            const ldouble* gg = L.g + (v * Hb + k - l) * 2;
             const double ex = L.ref[(v * Hb + k) * 2] - L.p0[(v * Hb + k) * 2];
             const double ey = L.ref[(v * Hb + k) * 2 + 1] - L.p0[(v * Hb + k) * 2 + 1];
             acc += qk * (gg[0] * ex + gg[1] * ey);
@@ -622,37 +619,51 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, Lay& L, int b) 
     return sflag;
 }
 
+// Out-of-line setup: the trigonometry and expm constants stay out of the
+// register allocation of the solve loop.
+template <bool HG, bool VG, int RM>
+__device__ __noinline__ int setup_problem_ni(const KArgs& a, gdouble* ws, int b, int Hb) {
+    const DevParams& P = *a.P;
+    const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
+    const Lay<HG, VG, RM> L = make_lay<HG, VG, RM>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
+    return setup_problem(a, P, L, b);
+}
+
 // ---------------------------------------------------------------------------
 // Structured linear operators (y-space = predicted-position space, [V][Hb][2])
 // ---------------------------------------------------------------------------
 // y[v][k] = sum_{l<=k} g[v][k-l] * x[v*Hb + l]     (calB x, MPC_Iter.py:146-147)
-__device__ __forceinline__ void toeplitz_apply(const Lay& L, const double* x, double* y) {
+template <class LT, class PX, class PY>
+__device__ __forceinline__ void toeplitz_apply(const LT& L, PX x, PY y) {
     for (int e = threadIdx.x; e < L.V * L.Hb; e += NT) {
         const int v = e / L.Hb, k = e % L.Hb;
-        const double* gv = L.g + v * L.Hb * 2;
-        const double* xv = x + v * L.Hb;
+        const ldouble* gv = L.g + v * L.Hb * 2;
+        const int xb = v * L.Hb;
         double a0 = 0.0, a1 = 0.0;
         for (int l = 0; l <= k; ++l) {
-            a0 += gv[(k - l) * 2] * xv[l];
-            a1 += gv[(k - l) * 2 + 1] * xv[l];
+            const double xl = x[xb + l];
+            a0 += gv[(k - l) * 2] * xl;
+            a1 += gv[(k - l) * 2 + 1] * xl;
         }
         y[2 * e] = a0;
         y[2 * e + 1] = a1;
     }
 }
 
-// out[v*Hb+l] = sum_{k>=l} g[v][k-l]' y[v][k]        (calB' y)
-__device__ __forceinline__ double toeplitz_t_entry(const Lay& L, const double* y, int v, int l) {
-    const double* gv = L.g + v * L.Hb * 2;
-    const double* yv = y + v * L.Hb * 2;
+// sum_{k>=l} g[v][k-l]' y[v][k]        (entry of calB' y)
+template <class LT, class PY>
+__device__ __forceinline__ double toeplitz_t_entry(const LT& L, PY y, int v, int l) {
+    const ldouble* gv = L.g + v * L.Hb * 2;
+    const int yb = v * L.Hb * 2;
     double acc = 0.0;
-    for (int k = l; k < L.Hb; ++k) acc += gv[(k - l) * 2] * yv[2 * k] + gv[(k - l) * 2 + 1] * yv[2 * k + 1];
+    for (int k = l; k < L.Hb; ++k)
+        acc += gv[(k - l) * 2] * y[yb + 2 * k] + gv[(k - l) * 2 + 1] * y[yb + 2 * k + 1];
     return acc;
 }
 
 // sum over the rows incident to (v, k) of coef(r) * sigma * e_r  (2-vector)
-template <class F>
-__device__ __forceinline__ void incident_sum(const Lay& L, int v, int k, F coef, double& s0,
+template <class LT, class F>
+__device__ __forceinline__ void incident_sum(const LT& L, int v, int k, F coef, double& s0,
                                             double& s1) {
     s0 = 0.0;
     s1 = 0.0;
@@ -672,15 +683,15 @@ __device__ __forceinline__ void incident_sum(const Lay& L, int v, int k, F coef,
     }
 }
 
-// Phase 2 of G x (needs ya = calB x_u):  out[i] = (G x)_i  (+ add[i] - h_i if given)
-__device__ __forceinline__ double gx_row(const Lay& L, const double* ya, const double* xu,
-                                         double xw, int r) {
+// (G x)_r given ya = calB x_u
+template <class LT, class PX>
+__device__ __forceinline__ double gx_row(const LT& L, PX xu, double xw, int r) {
     if (r < L.m) {
         int i, j, o, k;
-        row_decode(L, L.rinfo[r], i, j, o, k);
+        row_decode(L.rinfo[r], i, j, o, k);
         const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1];
-        double val = -(e0 * ya[(i * L.Hb + k) * 2] + e1 * ya[(i * L.Hb + k) * 2 + 1]);
-        if (j >= 0) val += e0 * ya[(j * L.Hb + k) * 2] + e1 * ya[(j * L.Hb + k) * 2 + 1];
+        double val = -(e0 * L.ya[(i * L.Hb + k) * 2] + e1 * L.ya[(i * L.Hb + k) * 2 + 1]);
+        if (j >= 0) val += e0 * L.ya[(j * L.Hb + k) * 2] + e1 * L.ya[(j * L.Hb + k) * 2 + 1];
         return val + L.rowW[r] * xw;
     }
     if (r < L.m + L.N) return xu[r - L.m];
@@ -688,8 +699,9 @@ __device__ __forceinline__ double gx_row(const Lay& L, const double* ya, const d
     return -xw;
 }
 
-// G' t: u-part into out[0..N), omega part returned (uniform).  Two phases.
-__device__ double gt_apply(const Lay& L, const double* t, double* out) {
+// G' t: u-part into out[0..N), omega part returned (uniform).
+template <class LT, class PT, class PO>
+__device__ double gt_apply(const LT& L, PT t, PO out) {
     const int tid = threadIdx.x;
     double wsum = 0.0;
     for (int e = tid; e < L.V * L.Hb; e += NT) {
@@ -701,7 +713,7 @@ __device__ double gt_apply(const Lay& L, const double* t, double* out) {
     }
     for (int r = tid; r < L.m; r += NT) wsum += t[r] * L.rowW[r];
     double red[4] = {wsum, 0.0, 0.0, 0.0};
-    block_reduce4(red, 0, L.red);   // includes barriers: yb visible afterwards
+    block_reduce4(red, 0, L.red);   // barriers: yb visible afterwards
     for (int e = tid; e < L.N; e += NT) {
         const int v = e / L.Hb, l = e % L.Hb;
         out[e] = toeplitz_t_entry(L, L.yb, v, l) + t[L.m + e] - t[L.m + L.N + e];
@@ -712,8 +724,8 @@ __device__ double gt_apply(const Lay& L, const double* t, double* out) {
 // ---------------------------------------------------------------------------
 // Normal matrix assembly  K = P_s + rho I + G' diag(d) G   (lower triangle)
 // ---------------------------------------------------------------------------
-template <bool HG>
-__device__ void assemble(const DevParams& P, const Lay& L, const double* d, double rho) {
+template <class LT, class PD>
+__device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb;
     const double u2 = P.uLim * P.uLim;
     // phase 1: W~ blocks [k][a>=b] (2x2) and the omega-coupling vector in y-space (yb)
@@ -724,7 +736,7 @@ __device__ void assemble(const DevParams& P, const Lay& L, const double* d, doub
             int a_ = 0;
             while ((a_ + 1) * (a_ + 2) / 2 <= ab) ++a_;
             const int b_ = ab - a_ * (a_ + 1) / 2;
-            double w00 = 0.0, w01 = 0.0, w10 = 0.0, w11 = 0.0;
+            double w00 = 0.0, w01 = 0.0, w11 = 0.0;
             if (a_ == b_) {
                 const double qk = 2.0 * u2 * ((k == Hb - 1) ? P.Qf[a_] : P.Q[a_]);
                 w00 = qk;
@@ -745,17 +757,15 @@ __device__ void assemble(const DevParams& P, const Lay& L, const double* d, doub
                     w01 += dr * e0 * e1;
                     w11 += dr * e1 * e1;
                 }
-                w10 = w01;
             } else {
                 const int r = pair_index(b_, a_, V) * Hb + k;   // b_ < a_
                 const double e0 = L.rowE[2 * r], e1 = L.rowE[2 * r + 1], dr = -d[r];
                 w00 = dr * e0 * e0;
                 w01 = dr * e0 * e1;
-                w10 = w01;
                 w11 = dr * e1 * e1;
             }
-            double* W = L.Wt + 4 * e;
-            W[0] = w00; W[1] = w01; W[2] = w10; W[3] = w11;
+            ldouble* W = L.Wt + 4 * e;
+            W[0] = w00; W[1] = w01; W[2] = w01; W[3] = w11;
         } else {
             const int q = e - nW, v = q / Hb, k = q % Hb;
             double s0, s1;
@@ -770,113 +780,287 @@ __device__ void assemble(const DevParams& P, const Lay& L, const double* d, doub
     block_reduce4(red, 0, L.red);
     // phase 2: K_uu lower triangle, omega row, omega diagonal
     const int N = L.N, ld = L.ld;
-    double* H = L.H;
     const int ty = tid >> 4, tx = tid & 15;
     for (int row = ty; row < N; row += 16) {
         const int a_ = row / Hb, l = row % Hb;
-        const double* ga = L.g + a_ * Hb * 2;
+        const ldouble* ga = L.g + a_ * Hb * 2;
         for (int col = tx; col <= row; col += 16) {
             const int b_ = col / Hb, lp = col % Hb;
-            const double* gb = L.g + b_ * Hb * 2;
+            const ldouble* gb = L.g + b_ * Hb * 2;
             const int k0 = l > lp ? l : lp;
-            const double* W = L.Wt + 4 * (k0 * nb + a_ * (a_ + 1) / 2 + b_);
-            double acc = 0.0;
-            for (int k = k0; k < Hb; ++k, W += 4 * nb) {
-                const double gb0 = gb[(k - lp) * 2], gb1 = gb[(k - lp) * 2 + 1];
-                const double t0 = W[0] * gb0 + W[1] * gb1;
-                const double t1 = W[2] * gb0 + W[3] * gb1;
-                acc += ga[(k - l) * 2] * t0 + ga[(k - l) * 2 + 1] * t1;
+            const ldouble* W = L.Wt + 4 * (k0 * nb + a_ * (a_ + 1) / 2 + b_);
+            double acc0 = 0.0, acc1 = 0.0;
+            int k = k0;
+            for (; k + 1 < Hb; k += 2, W += 8 * nb) {
+                const double2v ga0 = ld2(ga + (k - l) * 2), ga1 = ld2(ga + (k + 1 - l) * 2);
+                const double2v gb0 = ld2(gb + (k - lp) * 2), gb1 = ld2(gb + (k + 1 - lp) * 2);
+                const double2v w0 = ld2(W), w1 = ld2(W + 2);
+                const double2v v0 = ld2(W + 4 * nb), v1 = ld2(W + 4 * nb + 2);
+                acc0 += ga0.x * (w0.x * gb0.x + w0.y * gb0.y) + ga0.y * (w1.x * gb0.x + w1.y * gb0.y);
+                acc1 += ga1.x * (v0.x * gb1.x + v0.y * gb1.y) + ga1.y * (v1.x * gb1.x + v1.y * gb1.y);
             }
+            if (k < Hb) {
+                const double2v ga0 = ld2(ga + (k - l) * 2), gb0 = ld2(gb + (k - lp) * 2);
+                const double2v w0 = ld2(W), w1 = ld2(W + 2);
+                acc0 += ga0.x * (w0.x * gb0.x + w0.y * gb0.y) + ga0.y * (w1.x * gb0.x + w1.y * gb0.y);
+            }
+            double acc = acc0 + acc1;
             if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
-            H[row * ld + col] = acc;
+            L.H[row * ld + col] = acc;
         }
     }
     for (int e = tid; e < N; e += NT) {
         const int v = e / Hb, l = e % Hb;
-        H[N * ld + e] = toeplitz_t_entry(L, L.yb, v, l);
+        L.H[N * ld + e] = toeplitz_t_entry(L, L.yb, v, l);
     }
-    if (tid == 0) H[N * ld + N] = red[0] + d[L.mc - 1] + rho;
+    if (tid == 0) L.H[N * ld + N] = red[0] + d[L.mc - 1] + rho;
     __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// Cholesky  K = L L'  in place (lower), right-looking, one barrier per column
-// (column j-1 is scaled during step j).  Returns false on a non-positive pivot.
-// dinv[j] = 1 / L_jj.
+// Factorisation  K = L D L'  (L unit lower, stored strictly below the
+// diagonal of H; dvec = D, dinv = 1/D), blocked right-looking, panel width CB:
+//   1. wave 0 factors the n x CB panel in registers (pivots and panel-row
+//      entries broadcast with v_readlane: no barrier inside the panel);
+//   2. all 256 threads apply the rank-CB trailing update
+//      H_ik -= sum_c L_ic D_c L_kc in 2x2 register tiles with 16-byte loads.
+// Two barriers per panel, no square roots.  Returns false on a non-positive
+// pivot (K not numerically positive definite).
 // ---------------------------------------------------------------------------
-template <bool HG>
-__device__ bool cholesky(const Lay& L) {
+#define CB 8
+
+__device__ __forceinline__ bool wave0() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;   // wave-uniform branch
+}
+
+template <class LT>
+__device__ bool cholesky(const LT& L) {
     const int tid = threadIdx.x, n = L.n, ld = L.ld;
-    double* H = L.H;
     const int ty = tid >> 4, tx = tid & 15;
-    for (int j = 0; j < n; ++j) {
-        const double piv = H[j * ld + j];
-        if (!(piv > 0.0) || !isfinite(piv)) {
-            __syncthreads();
-            return false;
+    lint* flag = (lint*)(L.red + 62);
+    ldouble* dvec = L.red + 16;   // pivots of the current panel (8)
+    for (int j0 = 0; j0 < n; j0 += CB) {
+        const int jb = min(CB, n - j0);
+        if (wave0()) {
+            const int lane = tid;
+            double p[4][CB];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = j0 + lane + 64 * t;
+#pragma unroll
+                for (int c = 0; c < CB; c += 2) {
+                    double2v v = {0.0, 0.0};
+                    if (i < n && c < jb) v = ld2(L.H + i * ld + j0 + c);
+                    p[t][c] = v.x;
+                    p[t][c + 1] = v.y;
+                }
+            }
+            int bad = 0;
+#pragma unroll
+            for (int c = 0; c < CB; ++c) {
+                if (c < jb) {
+                    const double D = readlane_d(p[0][c], c);
+                    bad |= !(D > 0.0) || !isfinite(D);
+                    const double inv = 1.0 / D;
+#pragma unroll
+                    for (int c2 = c + 1; c2 < CB; ++c2) {
+                        if (c2 < jb) {
+                            const double lc = readlane_d(p[0][c], c2) * inv;
+#pragma unroll
+                            for (int t = 0; t < 4; ++t)
+                                if (lane + 64 * t >= c2) p[t][c2] -= p[t][c] * lc;
+                        }
+                    }
+#pragma unroll
+                    for (int t = 0; t < 4; ++t)
+                        if (lane + 64 * t > c) p[t][c] *= inv;
+                    if (lane == 0) {
+                        L.dinv[j0 + c] = inv;
+                        dvec[c] = D;
+                    }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int i = j0 + lane + 64 * t;
+                if (i < n) {
+#pragma unroll
+                    for (int c = 0; c < CB; ++c)
+                        if (c < jb && c <= lane + 64 * t) L.H[i * ld + j0 + c] = p[t][c];
+                }
+            }
+            if (lane == 0) flag[0] = bad;
         }
-        if (j > 0) {
-            const double sc = L.dinv[j - 1];
-            for (int i = j + tid; i < n; i += NT) H[i * ld + j - 1] *= sc;
+        __syncthreads();
+        if (flag[0]) return false;
+        const int r0 = j0 + jb;
+        if (r0 < n) {
+            double dc[CB];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) dc[c] = c < jb ? dvec[c] : 0.0;
+            const int T = (n - r0 + 1) >> 1;
+            for (int ti = ty; ti < T; ti += 16) {
+                const int i0 = r0 + 2 * ti, i1 = i0 + 1;
+                double a0[CB], a1[CB];
+#pragma unroll
+                for (int c = 0; c < CB; c += 2) {
+                    const double2v u = ld2(L.H + i0 * ld + j0 + c);
+                    double2v w = {0.0, 0.0};
+                    if (i1 < n) w = ld2(L.H + i1 * ld + j0 + c);
+                    a0[c] = u.x * dc[c]; a0[c + 1] = u.y * dc[c + 1];
+                    a1[c] = w.x * dc[c]; a1[c + 1] = w.y * dc[c + 1];
+                }
+                for (int tk = tx; tk <= ti; tk += 16) {
+                    const int k0 = r0 + 2 * tk, k1 = k0 + 1;
+                    double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
+#pragma unroll
+                    for (int c = 0; c < CB; c += 2) {
+                        const double2v u = ld2(L.H + k0 * ld + j0 + c);
+                        double2v w = {0.0, 0.0};
+                        if (k1 < n) w = ld2(L.H + k1 * ld + j0 + c);
+                        s00 += a0[c] * u.x + a0[c + 1] * u.y;
+                        s01 += a0[c] * w.x + a0[c + 1] * w.y;
+                        s10 += a1[c] * u.x + a1[c + 1] * u.y;
+                        s11 += a1[c] * w.x + a1[c + 1] * w.y;
+                    }
+                    L.H[i0 * ld + k0] -= s00;
+                    if (k1 <= i0) L.H[i0 * ld + k1] -= s01;
+                    if (i1 < n) {
+                        L.H[i1 * ld + k0] -= s10;
+                        if (k1 < n) L.H[i1 * ld + k1] -= s11;
+                    }
+                }
+            }
         }
-        const double rp = 1.0 / piv;
-        for (int i = j + 1 + ty; i < n; i += 16) {
-            const double lij = H[i * ld + j] * rp;
-            for (int k = j + 1 + tx; k <= i; k += 16) H[i * ld + k] -= lij * H[k * ld + j];
-        }
-        if (tid == 0) L.dinv[j] = 1.0 / sqrt(piv);
         __syncthreads();
     }
     return true;
 }
 
 // ---------------------------------------------------------------------------
-// Triangular solves with the factor: x = K^{-1} b.  Wave 0 only (column /
-// row oriented, pivots broadcast with v_readlane); rows i = lane + 64 t.
+// Solve K x = b with K = L D L'.  Wave 0 only; rows i = lane + 64 t (t < R).
+// Unit-lower forward / backward substitution: the dependency chain per step
+// is one v_readlane broadcast of the owner lane's value plus one FMA.  L is
+// streamed 8 columns (forward) / 8 rows (backward) at a time into registers,
+// double-buffered, so the LDS latency hides behind the dependent steps.
 // ---------------------------------------------------------------------------
-template <bool HG>
-__device__ void chol_solve(const Lay& L, const double* bvec, double* x) {
-    const int tid = threadIdx.x;
-    if (tid < 64) {
-        const int lane = tid, n = L.n, ld = L.ld;
-        const double* H = L.H;
-        double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-        if (lane < n) r0 = bvec[lane];
-        if (lane + 64 < n) r1 = bvec[lane + 64];
-        if (lane + 128 < n) r2 = bvec[lane + 128];
-        if (lane + 192 < n) r3 = bvec[lane + 192];
-        // forward: L y = b  (scaled column j is H[i][j] * dinv[j]; H holds L below the diagonal)
-        for (int j = 0; j < n; ++j) {
-            const int t = j >> 6, ln = j & 63;
-            double bj = (t == 0) ? r0 : (t == 1) ? r1 : (t == 2) ? r2 : r3;
-            const double xj = readlane_d(bj, ln) * L.dinv[j];
-            if (lane == ln) {
-                if (t == 0) r0 = xj; else if (t == 1) r1 = xj; else if (t == 2) r2 = xj; else r3 = xj;
-            }
-            const int i0 = lane, i1 = lane + 64, i2 = lane + 128, i3 = lane + 192;
-            if (i0 > j && i0 < n) r0 -= H[i0 * ld + j] * xj;
-            if (i1 > j && i1 < n) r1 -= H[i1 * ld + j] * xj;
-            if (i2 > j && i2 < n) r2 -= H[i2 * ld + j] * xj;
-            if (i3 > j && i3 < n) r3 -= H[i3 * ld + j] * xj;
+
+template <int R, class HP>
+struct Solver {
+    static constexpr int SCH = R <= 2 ? 8 : 4;   // chunk (columns / rows) streamed per step group
+    HP H;                   // factor (LDS or workspace)
+    const ldouble* dinv;
+    int lane, n, ld;
+    double r[R];
+    int ii[R];
+    double cur[R][SCH], nxt[R][SCH];
+
+    __device__ __forceinline__ Solver(HP H_, const ldouble* dinv_, int n_, int ld_,
+                                      const ldouble* bvec)
+        : H(H_), dinv(dinv_), n(n_), ld(ld_) {
+        lane = threadIdx.x & 63;
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            ii[t] = lane + 64 * t;
+            r[t] = ii[t] < n ? bvec[ii[t]] : 0.0;
         }
-        // backward: L' x = y
-        for (int j = n - 1; j >= 0; --j) {
-            const int t = j >> 6, ln = j & 63;
-            double bj = (t == 0) ? r0 : (t == 1) ? r1 : (t == 2) ? r2 : r3;
-            const double xj = readlane_d(bj, ln) * L.dinv[j];
-            if (lane == ln) {
-                if (t == 0) r0 = xj; else if (t == 1) r1 = xj; else if (t == 2) r2 = xj; else r3 = xj;
+    }
+    __device__ __forceinline__ void load_cols(double (&dst)[R][SCH], int jc) {
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+#pragma unroll
+            for (int q = 0; q < SCH; q += 2) {
+                double2v v = {0.0, 0.0};
+                if (ii[t] < n && jc + q < n) v = ld2(H + ii[t] * ld + jc + q);
+                dst[t][q] = (ii[t] > jc + q) ? v.x : 0.0;
+                dst[t][q + 1] = (ii[t] > jc + q + 1) ? v.y : 0.0;
             }
-            const double* Lr = H + j * ld;
-            if (lane < j) r0 -= Lr[lane] * xj;
-            if (lane + 64 < j) r1 -= Lr[lane + 64] * xj;
-            if (lane + 128 < j) r2 -= Lr[lane + 128] * xj;
-            if (lane + 192 < j) r3 -= Lr[lane + 192] * xj;
+    }
+    __device__ __forceinline__ void load_rows(double (&dst)[R][SCH], int jc) {
+#pragma unroll
+        for (int q = 0; q < SCH; ++q)
+#pragma unroll
+            for (int t = 0; t < R; ++t)
+                dst[t][q] = (jc + q < n && ii[t] < jc + q) ? H[(jc + q) * ld + ii[t]] : 0.0;
+    }
+    __device__ __forceinline__ void shift() {
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+#pragma unroll
+            for (int q = 0; q < SCH; ++q) cur[t][q] = nxt[t][q];
+    }
+    // forward over the columns owned by slot T (compile-time owner)
+    template <int T>
+    __device__ __forceinline__ void fwd() {
+        if constexpr (T < R) {
+            const int jend = min(n, 64 * (T + 1));
+            for (int jc = 64 * T; jc < jend; jc += SCH) {
+                if (jc + SCH < n) load_cols(nxt, jc + SCH);
+#pragma unroll
+                for (int q = 0; q < SCH; ++q) {
+                    const int j = jc + q;
+                    if (j < jend) {
+                        const double xj = readlane_d(r[T], j & 63);
+#pragma unroll
+                        for (int t = 0; t < R; ++t) r[t] -= cur[t][q] * xj;
+                    }
+                }
+                shift();
+            }
         }
-        if (lane < n) x[lane] = r0;
-        if (lane + 64 < n) x[lane + 64] = r1;
-        if (lane + 128 < n) x[lane + 128] = r2;
-        if (lane + 192 < n) x[lane + 192] = r3;
+    }
+    template <int T>
+    __device__ __forceinline__ void bwd(int jlast) {
+        if constexpr (T < R) {
+            const int jstart = (T == R - 1) ? jlast : 64 * T + 64 - SCH;
+            for (int jc = jstart; jc >= 64 * T; jc -= SCH) {
+                if (jc > 0) load_rows(nxt, jc - SCH);
+#pragma unroll
+                for (int q = SCH - 1; q >= 0; --q) {
+                    const int j = jc + q;
+                    if (j < n) {
+                        const double xj = readlane_d(r[T], j & 63);
+#pragma unroll
+                        for (int t = 0; t < R; ++t) r[t] -= cur[t][q] * xj;
+                    }
+                }
+                shift();
+            }
+        }
+    }
+    __device__ __forceinline__ void run(ldouble* x) {
+        // forward  L y = b
+        load_cols(cur, 0);
+        fwd<0>(); fwd<1>(); fwd<2>(); fwd<3>();
+        // z = D^{-1} y
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+            if (ii[t] < n) r[t] *= dinv[ii[t]];
+        // backward  L' x = z
+        const int jlast = ((n - 1) / SCH) * SCH;
+        load_rows(cur, jlast);
+        bwd<3>(jlast); bwd<2>(jlast); bwd<1>(jlast); bwd<0>(jlast);
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+            if (ii[t] < n) x[ii[t]] = r[t];
+    }
+};
+
+template <int R, class LT>
+__device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, ldouble* x) {
+    Solver<R, decltype(L.H)> S(L.H, L.dinv, L.n, L.ld, bvec);
+    S.run(x);
+}
+
+template <class LT>
+__device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
+    if (wave0()) {
+        const int n = L.n;
+        constexpr int RM = LT::RMAX;
+        if (RM == 1 || n <= 64) chol_solve_r<1>(L, bvec, x);
+        else if (RM == 2 || n <= 128) chol_solve_r<(RM >= 2 ? 2 : 1)>(L, bvec, x);
+        else if (RM == 3 || n <= 192) chol_solve_r<(RM >= 3 ? 3 : 1)>(L, bvec, x);
+        else chol_solve_r<RM>(L, bvec, x);
     }
     __syncthreads();
 }
@@ -891,7 +1075,8 @@ struct EvalRes {
     int feasible;
 };
 
-__device__ EvalRes evaluate_u(const DevParams& P, const Lay& L, const double* u, double* cveh,
+template <class LT>
+__device__ EvalRes evaluate_u(const DevParams& P, const LT& L, const ldouble* u, double* cveh,
                               double* cobs) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, O = L.O;
     toeplitz_apply(L, u, L.pb);
@@ -911,8 +1096,8 @@ __device__ EvalRes evaluate_u(const DevParams& P, const Lay& L, const double* u,
     const bool quirk = (P.flags & SCPQP_FLAG_OBST_QUIRK) != 0;
     for (int r = tid; r < L.m; r += NT) {
         int i, j, o, k;
-        row_decode(L, L.rinfo[r], i, j, o, k);
-        const double* pi = L.pb + (i * Hb + k) * 2;
+        row_decode(L.rinfo[r], i, j, o, k);
+        const ldouble* pi = L.pb + (i * Hb + k) * 2;
         double dx, dy, D2;
         if (j >= 0) {
             dx = pi[0] - L.pb[(j * Hb + k) * 2];
@@ -953,7 +1138,8 @@ __device__ EvalRes evaluate_u(const DevParams& P, const Lay& L, const double* u,
 //   e_r = 2 d uLim / nrm,  w_r = -1/nrm,  h_r = b_r / nrm,
 //   nrm = || [a_r uLim, -1] ||,  a_r = -2 d' calB_i,k (+ 2 d' calB_j,k)
 // ---------------------------------------------------------------------------
-__device__ void linearise_rows(const DevParams& P, const Lay& L) {
+template <class LT>
+__device__ void linearise_rows(const DevParams& P, const LT& L) {
     const int tid = threadIdx.x, Hb = L.Hb;
     toeplitz_apply(L, L.ub, L.ya);
     __syncthreads();
@@ -964,15 +1150,15 @@ __device__ void linearise_rows(const DevParams& P, const Lay& L) {
     __syncthreads();
     for (int r = tid; r < L.m; r += NT) {
         int i, j, o, k;
-        row_decode(L, L.rinfo[r], i, j, o, k);
-        const double* pi = L.pb + (i * Hb + k) * 2;
-        const double* yi = L.ya + (i * Hb + k) * 2;
+        row_decode(L.rinfo[r], i, j, o, k);
+        const ldouble* pi = L.pb + (i * Hb + k) * 2;
+        const ldouble* yi = L.ya + (i * Hb + k) * 2;
         double dx, dy, D2, au;
         if (j >= 0) {
             dx = pi[0] - L.pb[(j * Hb + k) * 2];
             dy = pi[1] - L.pb[(j * Hb + k) * 2 + 1];
             D2 = P.D2veh[i * SCPQP_MAX_VEH + j];
-            const double* yj = L.ya + (j * Hb + k) * 2;
+            const ldouble* yj = L.ya + (j * Hb + k) * 2;
             au = -2.0 * (dx * yi[0] + dy * yi[1]) + 2.0 * (dx * yj[0] + dy * yj[1]);
         } else {
             dx = pi[0] - L.ob[(o * Hb + k) * 2];
@@ -983,13 +1169,13 @@ __device__ void linearise_rows(const DevParams& P, const Lay& L) {
         const double c = D2 - (dx * dx + dy * dy);
         const double brow = -c + au;
         double a2 = 0.0;
-        const double* gi = L.g + i * Hb * 2;
+        const ldouble* gi = L.g + i * Hb * 2;
         for (int l = 0; l <= k; ++l) {
             const double t = dx * gi[(k - l) * 2] + dy * gi[(k - l) * 2 + 1];
             a2 += t * t;
         }
         if (j >= 0) {
-            const double* gj = L.g + j * Hb * 2;
+            const ldouble* gj = L.g + j * Hb * 2;
             for (int l = 0; l <= k; ++l) {
                 const double t = dx * gj[(k - l) * 2] + dy * gj[(k - l) * 2 + 1];
                 a2 += t * t;
@@ -1008,23 +1194,23 @@ __device__ void linearise_rows(const DevParams& P, const Lay& L) {
 // QP: Mehrotra predictor-corrector IPM + active-set polish, scaled variables.
 // x = L.z = [u~ (N), omega].  Returns IPM iterations; sets *qflags.
 // ---------------------------------------------------------------------------
-// G x  -> out (mc), phase structure: toeplitz into ya, then rows.
-__device__ void g_apply(const Lay& L, const double* x, double* out, const double* add_s,
-                        bool minus_h) {
+// out = G x (- h if minus_h)
+template <class LT, class PX, class PO>
+__device__ void g_apply(const LT& L, PX x, PO out, bool minus_h) {
     toeplitz_apply(L, x, L.ya);
     __syncthreads();
     const double xw = x[L.N];
     for (int r = threadIdx.x; r < L.mc; r += NT) {
-        double val = gx_row(L, L.ya, x, xw, r);
-        if (add_s) val += add_s[r];
+        double val = gx_row(L, x, xw, r);
         if (minus_h) val -= hval(L, r);
         out[r] = val;
     }
     __syncthreads();
 }
 
-// residuals rd (n), rp (mc) at (z, s, lam); returns {max|rp|, max|rd|, gap, pobj}
-__device__ void residuals(const DevParams& P, const Lay& L, double out[4]) {
+// residuals rd (n), rp (mc) at (z, s, lam); out = {max|rp|, max|rd|, gap, pobj}
+template <class LT>
+__device__ void residuals(const DevParams& P, const LT& L, double (&out)[4]) {
     const int tid = threadIdx.x, N = L.N, Hb = L.Hb;
     const double u2 = P.uLim * P.uLim;
     toeplitz_apply(L, L.z, L.ya);
@@ -1032,7 +1218,7 @@ __device__ void residuals(const DevParams& P, const Lay& L, double out[4]) {
     const double zw = L.z[N];
     double mrp = 0.0, gap = 0.0, wl = 0.0, quad = 0.0;
     for (int r = tid; r < L.mc; r += NT) {
-        const double v = gx_row(L, L.ya, L.z, zw, r) + L.s[r] - hval(L, r);
+        const double v = gx_row(L, L.z, zw, r) + L.s[r] - hval(L, r);
         L.rp[r] = v;
         mrp = fmax(mrp, fabs(v));
         gap += L.s[r] * L.lam[r];
@@ -1055,10 +1241,10 @@ __device__ void residuals(const DevParams& P, const Lay& L, double out[4]) {
         const int v = e / Hb, l = e % Hb;
         const double ze = L.z[e];
         const double pu = 2.0 * u2 * P.R[v] * ze;
-        const double v_ = toeplitz_t_entry(L, L.yb, v, l) + pu + L.qs[e] + L.lam[L.m + e] -
-                          L.lam[L.m + N + e];
-        L.rd[e] = v_;
-        mrd = fmax(mrd, fabs(v_));
+        const double rde = toeplitz_t_entry(L, L.yb, v, l) + pu + L.qs[e] + L.lam[L.m + e] -
+                           L.lam[L.m + N + e];
+        L.rd[e] = rde;
+        mrd = fmax(mrd, fabs(rde));
         quad2 += pu * ze;
         lin += L.qs[e] * ze;
     }
@@ -1073,7 +1259,8 @@ __device__ void residuals(const DevParams& P, const Lay& L, double out[4]) {
 }
 
 // max step keeping s + a ds >= 0, lam + a dl >= 0 (capped at 1)
-__device__ double max_step(const Lay& L) {
+template <class LT>
+__device__ double max_step(const LT& L) {
     double a = 1.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         if (L.ds[r] < 0.0) a = fmin(a, -L.s[r] / L.ds[r]);
@@ -1084,10 +1271,10 @@ __device__ double max_step(const Lay& L) {
     return -red[0];
 }
 
-// Newton direction for complementarity target rc (given through rc_of(r)):
+// Newton direction for complementarity target rc (rc_of(r)):
 //   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
-template <bool HG, class RC>
-__device__ void newton_dir(const Lay& L, RC rc_of) {
+template <class LT, class RC>
+__device__ void newton_dir(const LT& L, RC rc_of) {
     for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.dd[r] * L.rp[r] - rc_of(r) / L.s[r];
     __syncthreads();
     const double ow = gt_apply(L, L.tv, L.rhs);
@@ -1095,8 +1282,10 @@ __device__ void newton_dir(const Lay& L, RC rc_of) {
     __syncthreads();
     for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
     __syncthreads();
-    chol_solve<HG>(L, L.rhs, L.dz);
-    g_apply(L, L.dz, L.ds, nullptr, false);
+    PROF_T0();
+    chol_solve(L, L.rhs, L.dz);
+    PROF_ACC(9);
+    g_apply(L, L.dz, L.ds, false);
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double dsr = -L.rp[r] - L.ds[r];
         L.ds[r] = dsr;
@@ -1105,8 +1294,8 @@ __device__ void newton_dir(const Lay& L, RC rc_of) {
     __syncthreads();
 }
 
-template <bool HG>
-__device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
+template <class LT>
+__device__ int qp_solve(const DevParams& P, const LT& L, int* qflags) {
     const int tid = threadIdx.x, n = L.n, mc = L.mc, N = L.N;
     // ---- scale factors of the termination test
     double hmax = 1.0;
@@ -1125,35 +1314,30 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
         L.tv[r] = hval(L, r);
     }
     __syncthreads();
-    assemble<HG>(P, L, L.dd, 0.0);
-    cholesky<HG>(L);   // P + G'G is positive definite (box and omega rows)
+    assemble(P, L, L.dd, 0.0);
+    cholesky(L);   // P + G'G is positive definite (box and omega rows)
     {
         const double ow = gt_apply(L, L.tv, L.rhs);
         if (tid == 0) L.rhs[N] = ow - P.slackW;
         __syncthreads();
         for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e];
         __syncthreads();
-        chol_solve<HG>(L, L.rhs, L.z);
+        chol_solve(L, L.rhs, L.z);
     }
-    g_apply(L, L.z, L.s, nullptr, false);
-    double smin = 1e300, ssq = 0.0;
+    g_apply(L, L.z, L.s, false);
+    double smin = 1e300, ssq = 0.0, smax = -1e300;
     for (int r = tid; r < mc; r += NT) {
         const double sv = hval(L, r) - L.s[r];
         L.s[r] = sv;
         L.lam[r] = -sv;
         smin = fmin(smin, sv);
+        smax = fmax(smax, sv);
         ssq += sv * sv;
     }
     {
-        double red[4] = {-smin, ssq, 0.0, 0.0};
-        block_reduce4(red, 1, L.red);
-        const double ts = red[0], nrm = sqrt(red[1]);
-        // s shift (ts = -min s) and lam shift (tz = -min lam = max s)
-        double smax = -1e300;
-        for (int r = tid; r < mc; r += NT) smax = fmax(smax, -L.lam[r]);
-        double red2[4] = {smax, 0.0, 0.0, 0.0};
-        block_reduce4(red2, 1, L.red);
-        const double tz = red2[0];
+        double red[4] = {-smin, ssq, smax, 0.0};
+        block_reduce4(red, 5, L.red);
+        const double ts = red[0], nrm = sqrt(red[1]), tz = red[2];   // tz = -min(lam) = max(s)
         const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
         const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
         for (int r = tid; r < mc; r += NT) {
@@ -1165,9 +1349,12 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
     // ---- Mehrotra iterations
     int it = 0;
     bool conv = false;
+    PROF_T0();
     for (; it < P.maxIpm; ++it) {
         double res[4];
+        PROF_ACC(0);
         residuals(P, L, res);
+        PROF_ACC(1);
         if (res[0] <= P.ipmTol * hmax && res[1] <= P.ipmTol * qmax &&
             res[2] <= P.ipmTol * fmax(1.0, fabs(res[3]))) {
             conv = true;
@@ -1176,11 +1363,14 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
         const double mu = res[2] / mc;
         for (int r = tid; r < mc; r += NT) L.dd[r] = L.lam[r] / L.s[r];
         __syncthreads();
-        assemble<HG>(P, L, L.dd, 0.0);
-        if (!cholesky<HG>(L)) break;
+        assemble(P, L, L.dd, 0.0);
+        PROF_ACC(2);
+        if (!cholesky(L)) break;
+        PROF_ACC(3);
         // predictor (affine scaling): rc = s lam
-        newton_dir<HG>(L, [&](int r) { return L.s[r] * L.lam[r]; });
-        double aaff = max_step(L);
+        newton_dir(L, [&](int r) { return L.s[r] * L.lam[r]; });
+        PROF_ACC(4);
+        const double aaff = max_step(L);
         double mua = 0.0;
         for (int r = tid; r < mc; r += NT) {
             mua += (L.s[r] + aaff * L.ds[r]) * (L.lam[r] + aaff * L.dl[r]);
@@ -1190,10 +1380,10 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
         double red[4] = {mua, 0.0, 0.0, 0.0};
         block_reduce4(red, 0, L.red);
         const double sr = red[0] / mc / mu;
-        const double sigma = sr * sr * sr;
-        const double smu = sigma * mu;
+        const double smu = sr * sr * sr * mu;
         // corrector: rc = s lam + ds_aff dl_aff - sigma mu
-        newton_dir<HG>(L, [&](int r) { return L.s[r] * L.lam[r] + L.sa[r] * L.la[r] - smu; });
+        newton_dir(L, [&](int r) { return L.s[r] * L.lam[r] + L.sa[r] * L.la[r] - smu; });
+        PROF_ACC(5);
         const double alpha = fmin(1.0, 0.99 * max_step(L));
         for (int e = tid; e < n; e += NT) L.z[e] += alpha * L.dz[e];
         for (int r = tid; r < mc; r += NT) {
@@ -1201,6 +1391,7 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
             L.lam[r] += alpha * L.dl[r];
         }
         __syncthreads();
+        PROF_ACC(6);
     }
     if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
     // ---- active-set polish: proximal method of multipliers on {lam > s}
@@ -1213,8 +1404,12 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
     }
     for (int e = tid; e < n; e += NT) L.dz[e] = L.z[e];
     __syncthreads();
-    assemble<HG>(P, L, L.dd, rho);
-    bool ok = cholesky<HG>(L);
+#ifdef SCPQP_PROF
+    _pt = __builtin_amdgcn_s_memtime();
+#endif
+    assemble(P, L, L.dd, rho);
+    bool ok = cholesky(L);
+    PROF_ACC(7);
     if (ok) {
         for (int ref = 0; ref < P.nRefine; ++ref) {
             for (int r = tid; r < mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
@@ -1224,13 +1419,13 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
             __syncthreads();
             for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
             __syncthreads();
-            chol_solve<HG>(L, L.rhs, L.dz);
-            g_apply(L, L.dz, L.rp, nullptr, true);   // rp = G x - h
+            chol_solve(L, L.rhs, L.dz);
+            g_apply(L, L.dz, L.rp, true);   // rp = G x - h
             for (int r = tid; r < mc; r += NT)
                 if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
             __syncthreads();
         }
-        double viol = -1e300, ymin = 1e300, ymax = 0.0;
+        double viol = -1e300, ymin = 1e300, ymax = 0.0, nonfin = 0.0;
         for (int r = tid; r < mc; r += NT) {
             viol = fmax(viol, L.rp[r]);
             if (L.sa[r] != 0.0) {
@@ -1238,12 +1433,13 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
                 ymax = fmax(ymax, fabs(L.la[r]));
             }
         }
-        bool fin = true;
-        for (int e = tid; e < n; e += NT) fin = fin && isfinite(L.dz[e]);
-        double red[4] = {viol, -ymin, ymax, fin ? 0.0 : 1.0};
+        for (int e = tid; e < n; e += NT)
+            if (!isfinite(L.dz[e])) nonfin = 1.0;
+        double red[4] = {viol, -ymin, ymax, nonfin};
         block_reduce4(red, 15, L.red);
         ok = red[0] <= 1e-9 * hmax && -red[1] >= -1e-9 * fmax(1.0, red[2]) && red[3] == 0.0;
     }
+    PROF_ACC(8);
     if (ok) {
         for (int e = tid; e < n; e += NT) L.z[e] = L.dz[e];
     } else {
@@ -1256,25 +1452,26 @@ __device__ int qp_solve(const DevParams& P, const Lay& L, int* qflags) {
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
-template <bool HG, bool VG>
+template <bool HG, bool VG, int RM>
 __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
-    extern __shared__ double smem[];
+    ldouble* smem = (ldouble*)smem_;
     const DevParams& P = *a.P;
     const int tid = threadIdx.x;
-    double* ws = a.ws ? a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
+    gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
+    const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
+    lint* slot = (lint*)(smem + f.red + 60);
     for (;;) {
-        Lay L;
-        carve(&L, smem, ws, P.nV, P.nO, P.hpMax, P.hpMax, HG, VG);
-        int* slot = reinterpret_cast<int*>(L.red + 60);
         if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
         __syncthreads();
         const int b = slot[0];
         __syncthreads();
         if (b >= a.B) break;
         const int Hb = a.hp ? a.hp[b] : P.hpMax;
-        carve(&L, smem, ws, P.nV, P.nO, P.hpMax, Hb, HG, VG);
+        const Lay<HG, VG, RM> L = make_lay<HG, VG, RM>(smem, ws, f, P.nV, P.nO, Hb);
         const int V = L.V, N = L.N;
-        const int sflag = setup_problem(a, P, L, b);
+        PROF_T0();
+        const int sflag = setup_problem_ni<HG, VG, RM>(a, ws, b, Hb);
+        PROF_ACC(10);
         const int sflag_any = __syncthreads_or(sflag);
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
         if (a.mode == MODE_SAMPLE) {
@@ -1308,7 +1505,7 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
             if (co)
                 for (int i = tid; i < V * L.O * Hb; i += NT) co[i] = -INFINITY;
             __syncthreads();
-            EvalRes ev = evaluate_u(P, L, L.ub, cv, co);
+            const EvalRes ev = evaluate_u(P, L, L.ub, cv, co);
             if (tid == 0) {
                 if (a.obj) a.obj[b] = ev.obj;
                 if (a.maxv) a.maxv[b] = ev.maxv;
@@ -1333,8 +1530,10 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
         const int maxScp = a.maxScp > 0 ? a.maxScp : P.maxScp;
         int qflags = 0, nipm = 0, it = 0, status = SCPQP_ST_MAX_SCP;
         for (it = 0; it < maxScp; ++it) {
+            PROF_T0();
             linearise_rows(P, L);
-            nipm += qp_solve<HG>(P, L, &qflags);
+            PROF_ACC(11);
+            nipm += qp_solve(P, L, &qflags);
             for (int i = tid; i < N; i += NT) L.ub[i] = P.uLim * L.z[i];
             __syncthreads();
             ev = evaluate_u(P, L, L.ub, nullptr, nullptr);
@@ -1387,9 +1586,9 @@ int fail(int code, const char* fmt, const char* detail = "") {
     return code;
 }
 
-#define HIPCHK(x)                                                               \
-    do {                                                                        \
-        hipError_t e_ = (x);                                                    \
+#define HIPCHK(x)                                                                          \
+    do {                                                                                   \
+        hipError_t e_ = (x);                                                               \
         if (e_ != hipSuccess) return fail(SCPQP_E_HIP, "HIP error: %s", hipGetErrorString(e_)); \
     } while (0)
 
@@ -1418,13 +1617,13 @@ int plan(scpqp_handle* h) {
     const int V = h->dims.n_veh, O = h->dims.n_obst, Hm = h->dims.hp_max;
     for (int cfg = 0; cfg < 3; ++cfg) {
         const bool hG = cfg >= 2, vG = cfg >= 1;
-        Sizes S = carve(nullptr, nullptr, nullptr, V, O, Hm, Hm, hG, vG);
-        const size_t lds = (size_t)(S.persist + S.uni) * sizeof(double);
+        const Off f = plan_offsets(V, O, Hm, hG, vG);
+        const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
         if (lds <= kLdsLimit) {
             h->hG = hG;
             h->vG = vG;
             h->ldsBytes = lds;
-            h->wsStride = S.ws;
+            h->wsStride = f.ws;
             int perCU = (int)(kLdsLimit / lds);
             if (perCU > 8) perCU = 8;
             if (perCU < 1) perCU = 1;
@@ -1435,9 +1634,9 @@ int plan(scpqp_handle* h) {
     return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
 }
 
-template <bool HG, bool VG>
+template <bool HG, bool VG, int RM>
 int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
-    auto kern = scp_kernel<HG, VG>;
+    auto kern = scp_kernel<HG, VG, RM>;
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->ldsBytes));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), h->ldsBytes, st, a);
@@ -1448,7 +1647,7 @@ int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
 int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     if (a.B <= 0) return 0;
     HIPCHK(hipSetDevice(h->device));
-    int grid = a.B < h->grid ? a.B : h->grid;
+    const int grid = a.B < h->grid ? a.B : h->grid;
     if (h->wsStride > 0) {
         const size_t need = (size_t)grid * h->wsStride * sizeof(double);
         if (need > h->wsBytes) {
@@ -1463,9 +1662,18 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.wsStride = h->wsStride;
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
-    if (h->hG) return launch_t<true, true>(h, a, st, grid);
-    if (h->vG) return launch_t<false, true>(h, a, st, grid);
-    return launch_t<false, false>(h, a, st, grid);
+    const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
+#define SCPQP_DISPATCH(HGV, VGV)                                              \
+    switch (R) {                                                             \
+        case 1: return launch_t<HGV, VGV, 1>(h, a, st, grid);                \
+        case 2: return launch_t<HGV, VGV, 2>(h, a, st, grid);                \
+        case 3: return launch_t<HGV, VGV, 3>(h, a, st, grid);                \
+        default: return launch_t<HGV, VGV, 4>(h, a, st, grid);               \
+    }
+    if (h->hG) { SCPQP_DISPATCH(true, true) }
+    if (h->vG) { SCPQP_DISPATCH(false, true) }
+    SCPQP_DISPATCH(false, false)
+#undef SCPQP_DISPATCH
 }
 
 int check_in(scpqp_handle* h, int32_t B, const scpqp_batch_in* in) {
@@ -1497,7 +1705,7 @@ extern "C" {
 
 const char* scpqp_last_error(void) { return g_err; }
 
-const char* scpqp_version(void) { return "scpqp-mi355x 0.1 (gfx950, fp64)"; }
+const char* scpqp_version(void) { return "scpqp-mi355x 0.2 (gfx950, fp64)"; }
 
 int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpqp_handle** out) {
     if (!dims || !p || !out) return fail(SCPQP_E_ARG, "null argument%s");
@@ -1565,7 +1773,7 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
         scpqp_destroy(h);
         return SCPQP_E_HIP;
     }
-    int rc = plan(h);
+    const int rc = plan(h);
     if (rc) {
         scpqp_destroy(h);
         return rc;
@@ -1586,7 +1794,7 @@ int scpqp_destroy(scpqp_handle* h) {
 
 int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_batch_out* out,
                 void* stream) {
-    int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in);
     if (rc) return rc;
     if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
     KArgs a = base_args(B, in);
@@ -1605,7 +1813,7 @@ int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpq
 
 int scpqp_linearize(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_lin_out* out,
                     void* stream) {
-    int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in);
     if (rc) return rc;
     if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
     KArgs a = base_args(B, in);
@@ -1622,7 +1830,7 @@ int scpqp_linearize(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const 
 
 int scpqp_evaluate(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const double* u,
                    const scpqp_eval_out* out, void* stream) {
-    int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in);
     if (rc) return rc;
     if (!out || !u) return fail(SCPQP_E_ARG, "null u or output struct%s");
     KArgs a = base_args(B, in);
@@ -1640,7 +1848,7 @@ int scpqp_evaluate(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const d
 
 int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, double* ref,
                            void* stream) {
-    int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in);
     if (rc) return rc;
     if (!ref) return fail(SCPQP_E_ARG, "null ref_points%s");
     KArgs a = base_args(B, in);
@@ -1649,6 +1857,17 @@ int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in,
     a.refOut = ref;
     return launch(h, a, static_cast<hipStream_t>(stream));
 }
+
+#ifdef SCPQP_PROF
+int scpqp_prof_read(unsigned long long* out, int reset) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+    if (reset) {
+        unsigned long long z[16] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+    }
+    return 0;
+}
+#endif
 
 int scpqp_resources(scpqp_handle* h, int64_t* lds, int64_t* ws, int32_t* big, int32_t* grid) {
     if (!h) return fail(SCPQP_E_ARG, "null handle%s");

@@ -79,6 +79,12 @@ def run(nv, hp, B, nchk, mixed=None):
             continue
         eu = max(eu, float(np.max(np.abs(u.cpu().numpy() - r.u))))
         et = max(et, float(np.max(np.abs(tr.cpu().numpy() - r.traj))))
+    ts = []
+    for _ in range(3):
+        torch.cuda.synchronize(); t = time.time()
+        S.solve(bt.x0, bt.u0, bt.ec_noise, hp=hpa, out=out)
+        torch.cuda.synchronize(); ts.append(time.time() - t)
+    dt = min(ts)
     st = out.status.cpu().numpy()
     print(f"  full SCP: u err {eu:.1e} traj err {et:.1e} nscp-mismatch {mism}/{nchk}; "
           f"status hist {np.unique(st, return_counts=True)}; nscp mean {out.n_scp.float().mean().item():.2f} "

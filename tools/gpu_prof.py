@@ -1,0 +1,32 @@
+"""Phase-stamp breakdown (diagnostic build libscpqp_prof.so): cycles of workgroup 0."""
+import os, sys, ctypes as C, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd")
+sys.path.insert(0, PKG)
+import numpy as np, torch
+from scpqp import _lib as LB
+lib = LB.load(os.path.join(PKG, "scpqp", "libscpqp_prof.so"))
+LB._lib = lib
+lib.scpqp_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+from oracle import scp_reference as R
+from scpqp import batch as BT
+from scpqp.solver import ScpQpSolver
+names = ["ipm-loop-top", "residuals", "assemble", "cholesky", "newton(pred)", "maxstep+corr",
+         "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise"]
+for nv, hp, B in [(4, 20, 1), (8, 30, 1)]:
+    sc = R.circle_scenario(nv, Hp=hp)
+    bt = BT.make_batch(sc, B, base_seed=1000)
+    S = ScpQpSolver(sc, max_batch=B)
+    S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
+    buf = (C.c_ulonglong * 16)()
+    lib.scpqp_prof_read(buf, 1)
+    t = time.time()
+    out = S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
+    wall = time.time() - t
+    lib.scpqp_prof_read(buf, 1)
+    tot = sum(buf[i] for i in range(12) if i != 9)
+    nipm = out.n_ipm[0].item()
+    print(f"nv={nv} hp={hp}: wall {wall*1e3:.2f} ms, nscp {out.n_scp[0].item()} nipm {nipm}")
+    for i, nme in enumerate(names):
+        print(f"   {nme:15s} {buf[i]:12d} cyc  {buf[i]/max(nipm,1):10.0f}/ipm-it")
