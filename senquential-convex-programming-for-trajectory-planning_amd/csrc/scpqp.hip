@@ -44,7 +44,12 @@
 
 #include "scpqp.h"
 
-#define NT 256
+#ifndef SCPQP_NT
+#define SCPQP_NT 256
+#endif
+#define NT SCPQP_NT
+#define TXD 16            // column stride of the 2-D thread grid
+#define TYD (NT / TXD)    // row stride
 #define NWAVE (NT / 64)
 #define SCR_PER_WAVE 640
 
@@ -116,6 +121,10 @@ struct KArgs {
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int pad2(int x) { return (x + 1) & ~1; }
 
+// Packed lower-triangular storage of the KKT matrix: row i holds columns 0..i,
+// padded to an even length so every row starts 16-byte aligned.
+__host__ __device__ __forceinline__ int roff(int i) { return i * (i + 1) / 2 + ((i + 1) >> 1); }
+
 struct Off {
     int x0, u0, ec, g, p0, ref, ob, ub, pb, ya, yb, qs, rowE, rowW, rowH, rinfo;
     int z, dz, rhs, rd, dinv, red, scr;
@@ -150,11 +159,11 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.rhs = p; p += pad2(n);
     f.rd = p; p += pad2(n);
     f.dinv = p; p += pad2(n);
-    f.red = p; p += 64;
+    f.red = p; p += 128;   // [0,64) reductions, [64,80) panel pivots, 120 flag, 124 work slot
     f.persist = p;
     f.scr = p;
     int u = 0, w = 0;
-    if (hG) { f.H = w; w += pad2(n * ld); } else { f.H = p + u; u += pad2(n * ld); }
+    if (hG) { f.H = w; w += pad2(roff(n) + 16); } else { f.H = p + u; u += pad2(roff(n) + 16); }
     f.Wt = p + u; u += pad2(4 * Hm * nb);
     if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     const int setup = NWAVE * SCR_PER_WAVE;
@@ -780,11 +789,11 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
     block_reduce4(red, 0, L.red);
     // phase 2: K_uu lower triangle, omega row, omega diagonal
     const int N = L.N, ld = L.ld;
-    const int ty = tid >> 4, tx = tid & 15;
-    for (int row = ty; row < N; row += 16) {
+    const int ty = tid / TXD, tx = tid % TXD;
+    for (int row = ty; row < N; row += TYD) {
         const int a_ = row / Hb, l = row % Hb;
         const ldouble* ga = L.g + a_ * Hb * 2;
-        for (int col = tx; col <= row; col += 16) {
+        for (int col = tx; col <= row; col += TXD) {
             const int b_ = col / Hb, lp = col % Hb;
             const ldouble* gb = L.g + b_ * Hb * 2;
             const int k0 = l > lp ? l : lp;
@@ -806,14 +815,14 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
             }
             double acc = acc0 + acc1;
             if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
-            L.H[row * ld + col] = acc;
+            L.H[roff(row) + col] = acc;
         }
     }
     for (int e = tid; e < N; e += NT) {
         const int v = e / Hb, l = e % Hb;
-        L.H[N * ld + e] = toeplitz_t_entry(L, L.yb, v, l);
+        L.H[roff(N) + e] = toeplitz_t_entry(L, L.yb, v, l);
     }
-    if (tid == 0) L.H[N * ld + N] = red[0] + d[L.mc - 1] + rho;
+    if (tid == 0) L.H[roff(N) + N] = red[0] + d[L.mc - 1] + rho;
     __syncthreads();
 }
 
@@ -836,21 +845,22 @@ __device__ __forceinline__ bool wave0() {
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int tid = threadIdx.x, n = L.n, ld = L.ld;
-    const int ty = tid >> 4, tx = tid & 15;
-    lint* flag = (lint*)(L.red + 62);
-    ldouble* dvec = L.red + 16;   // pivots of the current panel (8)
+    const int ty = tid / TXD, tx = tid % TXD;
+    constexpr int RS = LT::RMAX;   // row slots per lane in the panel
+    lint* flag = (lint*)(L.red + 120);
+    ldouble* dvec = L.red + 64;   // pivots of the current panel (CB)
     for (int j0 = 0; j0 < n; j0 += CB) {
         const int jb = min(CB, n - j0);
         if (wave0()) {
             const int lane = tid;
-            double p[4][CB];
+            double p[RS][CB];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < RS; ++t) {
                 const int i = j0 + lane + 64 * t;
 #pragma unroll
                 for (int c = 0; c < CB; c += 2) {
                     double2v v = {0.0, 0.0};
-                    if (i < n && c < jb) v = ld2(L.H + i * ld + j0 + c);
+                    if (i < n && c < jb) v = ld2(L.H + roff(i) + j0 + c);
                     p[t][c] = v.x;
                     p[t][c + 1] = v.y;
                 }
@@ -867,12 +877,12 @@ __device__ bool cholesky(const LT& L) {
                         if (c2 < jb) {
                             const double lc = readlane_d(p[0][c], c2) * inv;
 #pragma unroll
-                            for (int t = 0; t < 4; ++t)
+                            for (int t = 0; t < RS; ++t)
                                 if (lane + 64 * t >= c2) p[t][c2] -= p[t][c] * lc;
                         }
                     }
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
+                    for (int t = 0; t < RS; ++t)
                         if (lane + 64 * t > c) p[t][c] *= inv;
                     if (lane == 0) {
                         L.dinv[j0 + c] = inv;
@@ -881,12 +891,12 @@ __device__ bool cholesky(const LT& L) {
                 }
             }
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
+            for (int t = 0; t < RS; ++t) {
                 const int i = j0 + lane + 64 * t;
                 if (i < n) {
 #pragma unroll
                     for (int c = 0; c < CB; ++c)
-                        if (c < jb && c <= lane + 64 * t) L.H[i * ld + j0 + c] = p[t][c];
+                        if (c < jb && c <= lane + 64 * t) L.H[roff(i) + j0 + c] = p[t][c];
                 }
             }
             if (lane == 0) flag[0] = bad;
@@ -899,35 +909,37 @@ __device__ bool cholesky(const LT& L) {
 #pragma unroll
             for (int c = 0; c < CB; ++c) dc[c] = c < jb ? dvec[c] : 0.0;
             const int T = (n - r0 + 1) >> 1;
-            for (int ti = ty; ti < T; ti += 16) {
+            for (int ti = ty; ti < T; ti += TYD) {
                 const int i0 = r0 + 2 * ti, i1 = i0 + 1;
+                const int o0 = roff(i0), o1 = roff(i1);
                 double a0[CB], a1[CB];
 #pragma unroll
                 for (int c = 0; c < CB; c += 2) {
-                    const double2v u = ld2(L.H + i0 * ld + j0 + c);
+                    const double2v u = ld2(L.H + o0 + j0 + c);
                     double2v w = {0.0, 0.0};
-                    if (i1 < n) w = ld2(L.H + i1 * ld + j0 + c);
+                    if (i1 < n) w = ld2(L.H + o1 + j0 + c);
                     a0[c] = u.x * dc[c]; a0[c + 1] = u.y * dc[c + 1];
                     a1[c] = w.x * dc[c]; a1[c + 1] = w.y * dc[c + 1];
                 }
-                for (int tk = tx; tk <= ti; tk += 16) {
+                for (int tk = tx; tk <= ti; tk += TXD) {
                     const int k0 = r0 + 2 * tk, k1 = k0 + 1;
+                    const int q0 = roff(k0), q1 = roff(k1);
                     double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
 #pragma unroll
                     for (int c = 0; c < CB; c += 2) {
-                        const double2v u = ld2(L.H + k0 * ld + j0 + c);
+                        const double2v u = ld2(L.H + q0 + j0 + c);
                         double2v w = {0.0, 0.0};
-                        if (k1 < n) w = ld2(L.H + k1 * ld + j0 + c);
+                        if (k1 < n) w = ld2(L.H + q1 + j0 + c);
                         s00 += a0[c] * u.x + a0[c + 1] * u.y;
                         s01 += a0[c] * w.x + a0[c + 1] * w.y;
                         s10 += a1[c] * u.x + a1[c + 1] * u.y;
                         s11 += a1[c] * w.x + a1[c + 1] * w.y;
                     }
-                    L.H[i0 * ld + k0] -= s00;
-                    if (k1 <= i0) L.H[i0 * ld + k1] -= s01;
+                    L.H[o0 + k0] -= s00;
+                    if (k1 <= i0) L.H[o0 + k1] -= s01;
                     if (i1 < n) {
-                        L.H[i1 * ld + k0] -= s10;
-                        if (k1 < n) L.H[i1 * ld + k1] -= s11;
+                        L.H[o1 + k0] -= s10;
+                        if (k1 < n) L.H[o1 + k1] -= s11;
                     }
                 }
             }
@@ -952,7 +964,7 @@ struct Solver {
     const ldouble* dinv;
     int lane, n, ld;
     double r[R];
-    int ii[R];
+    int ii[R], ro[R];
     double cur[R][SCH], nxt[R][SCH];
 
     __device__ __forceinline__ Solver(HP H_, const ldouble* dinv_, int n_, int ld_,
@@ -962,6 +974,7 @@ struct Solver {
 #pragma unroll
         for (int t = 0; t < R; ++t) {
             ii[t] = lane + 64 * t;
+            ro[t] = roff(ii[t]);
             r[t] = ii[t] < n ? bvec[ii[t]] : 0.0;
         }
     }
@@ -971,7 +984,7 @@ struct Solver {
 #pragma unroll
             for (int q = 0; q < SCH; q += 2) {
                 double2v v = {0.0, 0.0};
-                if (ii[t] < n && jc + q < n) v = ld2(H + ii[t] * ld + jc + q);
+                if (ii[t] < n && jc + q < n) v = ld2(H + ro[t] + jc + q);
                 dst[t][q] = (ii[t] > jc + q) ? v.x : 0.0;
                 dst[t][q + 1] = (ii[t] > jc + q + 1) ? v.y : 0.0;
             }
@@ -981,7 +994,7 @@ struct Solver {
         for (int q = 0; q < SCH; ++q)
 #pragma unroll
             for (int t = 0; t < R; ++t)
-                dst[t][q] = (jc + q < n && ii[t] < jc + q) ? H[(jc + q) * ld + ii[t]] : 0.0;
+                dst[t][q] = (jc + q < n && ii[t] < jc + q) ? H[roff(jc + q) + ii[t]] : 0.0;
     }
     __device__ __forceinline__ void shift() {
 #pragma unroll
@@ -1282,9 +1295,7 @@ __device__ void newton_dir(const LT& L, RC rc_of) {
     __syncthreads();
     for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
     __syncthreads();
-    PROF_T0();
     chol_solve(L, L.rhs, L.dz);
-    PROF_ACC(9);
     g_apply(L, L.dz, L.ds, false);
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double dsr = -L.rp[r] - L.ds[r];
@@ -1294,39 +1305,93 @@ __device__ void newton_dir(const LT& L, RC rc_of) {
     __syncthreads();
 }
 
-template <class LT>
-__device__ int qp_solve(const DevParams& P, const LT& L, int* qflags) {
-    const int tid = threadIdx.x, n = L.n, mc = L.mc, N = L.N;
-    // ---- scale factors of the termination test
+// ---------------------------------------------------------------------------
+// Phase functions.  Each is deliberately out of line and takes a 3-scalar
+// context from which it rebuilds the LDS layout (a few integer ops), so every
+// phase is register-allocated on its own and the IPM driver keeps only a few
+// scalars live.  (One monolithic inlined body needed ~450 registers.)
+// ---------------------------------------------------------------------------
+struct Ctx {
+    const DevParams* P;
+    gdouble* ws;
+    int Hb;
+};
+struct D4 {
+    double a, b, c, d;
+};
+
+template <bool HG, bool VG, int RM>
+__device__ __forceinline__ Lay<HG, VG, RM> lay_of(const Ctx& c) {
+    const Off f = plan_offsets(c.P->nV, c.P->nO, c.P->hpMax, HG, VG);
+    return make_lay<HG, VG, RM>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
+}
+#define PHASE template <bool HG, bool VG, int RM> __device__ __noinline__
+#define LAYDEF                  \
+    const DevParams& P = *c.P;  \
+    const Lay<HG, VG, RM> L = lay_of<HG, VG, RM>(c); \
+    (void)P
+#define PH(f) f<HG, VG, RM>
+
+PHASE void ph_assemble(Ctx c, double rho) {
+    LAYDEF;
+    assemble(P, L, L.dd, rho);
+}
+PHASE int ph_cholesky(Ctx c) {
+    LAYDEF;
+    return cholesky(L) ? 1 : 0;
+}
+// x = K^{-1} rhs into z (dst = 0) or dz (dst = 1)
+PHASE void ph_solve(Ctx c, int dst) {
+    LAYDEF;
+    chol_solve(L, L.rhs, dst ? L.dz : L.z);
+}
+PHASE void ph_linearise(Ctx c) {
+    LAYDEF;
+    linearise_rows(P, L);
+}
+PHASE EvalRes ph_evaluate(Ctx c, double* cveh, double* cobs) {
+    LAYDEF;
+    return evaluate_u(P, L, L.ub, cveh, cobs);
+}
+PHASE D4 ph_residuals(Ctx c) {
+    LAYDEF;
+    double r[4];
+    residuals(P, L, r);
+    return D4{r[0], r[1], r[2], r[3]};
+}
+// rhs = -q + G'(tv) with tv = h (init) or tv = mask (h/delta - y) (polish), + rho x_k
+PHASE void ph_rhs_from_tv(Ctx c, double rho) {
+    LAYDEF;
+    const double ow = gt_apply(L, L.tv, L.rhs);
+    if (threadIdx.x == 0) L.rhs[L.N] = ow - P.slackW + rho * L.dz[L.N];
+    __syncthreads();
+    for (int e = threadIdx.x; e < L.N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
+    __syncthreads();
+}
+// scale factors of the termination test + initial-point setup of dd/tv
+PHASE D4 ph_init_a(Ctx c) {
+    LAYDEF;
+    const int tid = threadIdx.x;
     double hmax = 1.0;
     for (int r = tid; r < L.m; r += NT) hmax = fmax(hmax, fabs(L.rowH[r]));
     double qmax = fmax(1.0, P.slackW);
-    for (int e = tid; e < N; e += NT) qmax = fmax(qmax, fabs(L.qs[e]));
-    {
-        double red[4] = {hmax, qmax, 0.0, 0.0};
-        block_reduce4(red, 3, L.red);
-        hmax = red[0];
-        qmax = red[1];
-    }
-    // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
-    for (int r = tid; r < mc; r += NT) {
+    for (int e = tid; e < L.N; e += NT) qmax = fmax(qmax, fabs(L.qs[e]));
+    for (int r = tid; r < L.mc; r += NT) {
         L.dd[r] = 1.0;
         L.tv[r] = hval(L, r);
     }
-    __syncthreads();
-    assemble(P, L, L.dd, 0.0);
-    cholesky(L);   // P + G'G is positive definite (box and omega rows)
-    {
-        const double ow = gt_apply(L, L.tv, L.rhs);
-        if (tid == 0) L.rhs[N] = ow - P.slackW;
-        __syncthreads();
-        for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e];
-        __syncthreads();
-        chol_solve(L, L.rhs, L.z);
-    }
+    for (int e = tid; e < L.n; e += NT) L.dz[e] = 0.0;
+    double red[4] = {hmax, qmax, 0.0, 0.0};
+    block_reduce4(red, 3, L.red);
+    return D4{red[0], red[1], 0.0, 0.0};
+}
+// s = h - G z, lam = -s, CVXOPT positivity shifts
+PHASE void ph_init_b(Ctx c) {
+    LAYDEF;
+    const int tid = threadIdx.x;
     g_apply(L, L.z, L.s, false);
     double smin = 1e300, ssq = 0.0, smax = -1e300;
-    for (int r = tid; r < mc; r += NT) {
+    for (int r = tid; r < L.mc; r += NT) {
         const double sv = hval(L, r) - L.s[r];
         L.s[r] = sv;
         L.lam[r] = -sv;
@@ -1334,118 +1399,200 @@ __device__ int qp_solve(const DevParams& P, const LT& L, int* qflags) {
         smax = fmax(smax, sv);
         ssq += sv * sv;
     }
-    {
-        double red[4] = {-smin, ssq, smax, 0.0};
-        block_reduce4(red, 5, L.red);
-        const double ts = red[0], nrm = sqrt(red[1]), tz = red[2];   // tz = -min(lam) = max(s)
-        const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
-        const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
-        for (int r = tid; r < mc; r += NT) {
-            if (shs) L.s[r] += 1.0 + ts;
-            if (shz) L.lam[r] += 1.0 + tz;
-        }
-        __syncthreads();
+    double red[4] = {-smin, ssq, smax, 0.0};
+    block_reduce4(red, 5, L.red);
+    const double ts = red[0], nrm = sqrt(red[1]), tz = red[2];   // tz = -min(lam) = max(s)
+    const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
+    const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
+    for (int r = tid; r < L.mc; r += NT) {
+        if (shs) L.s[r] += 1.0 + ts;
+        if (shz) L.lam[r] += 1.0 + tz;
     }
-    // ---- Mehrotra iterations
-    int it = 0;
-    bool conv = false;
-    PROF_T0();
-    for (; it < P.maxIpm; ++it) {
-        double res[4];
-        PROF_ACC(0);
-        residuals(P, L, res);
-        PROF_ACC(1);
-        if (res[0] <= P.ipmTol * hmax && res[1] <= P.ipmTol * qmax &&
-            res[2] <= P.ipmTol * fmax(1.0, fabs(res[3]))) {
-            conv = true;
-            break;
-        }
-        const double mu = res[2] / mc;
-        for (int r = tid; r < mc; r += NT) L.dd[r] = L.lam[r] / L.s[r];
-        __syncthreads();
-        assemble(P, L, L.dd, 0.0);
-        PROF_ACC(2);
-        if (!cholesky(L)) break;
-        PROF_ACC(3);
-        // predictor (affine scaling): rc = s lam
-        newton_dir(L, [&](int r) { return L.s[r] * L.lam[r]; });
-        PROF_ACC(4);
-        const double aaff = max_step(L);
-        double mua = 0.0;
-        for (int r = tid; r < mc; r += NT) {
-            mua += (L.s[r] + aaff * L.ds[r]) * (L.lam[r] + aaff * L.dl[r]);
-            L.sa[r] = L.ds[r];
-            L.la[r] = L.dl[r];
-        }
-        double red[4] = {mua, 0.0, 0.0, 0.0};
-        block_reduce4(red, 0, L.red);
-        const double sr = red[0] / mc / mu;
-        const double smu = sr * sr * sr * mu;
-        // corrector: rc = s lam + ds_aff dl_aff - sigma mu
-        newton_dir(L, [&](int r) { return L.s[r] * L.lam[r] + L.sa[r] * L.la[r] - smu; });
-        PROF_ACC(5);
-        const double alpha = fmin(1.0, 0.99 * max_step(L));
-        for (int e = tid; e < n; e += NT) L.z[e] += alpha * L.dz[e];
-        for (int r = tid; r < mc; r += NT) {
-            L.s[r] += alpha * L.ds[r];
-            L.lam[r] += alpha * L.dl[r];
-        }
-        __syncthreads();
-        PROF_ACC(6);
+    __syncthreads();
+}
+PHASE void ph_scaling(Ctx c) {
+    LAYDEF;
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] / L.s[r];
+    __syncthreads();
+}
+// Newton direction, complementarity target rc = s lam (+ ds_aff dl_aff - smu if corr):
+//   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
+PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
+    LAYDEF;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
+        L.tv[r] = L.dd[r] * L.rp[r] - rc / L.s[r];
     }
-    if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
-    // ---- active-set polish: proximal method of multipliers on {lam > s}
-    const double idl = 1.0 / P.polDelta, rho = P.polRho;
-    for (int r = tid; r < mc; r += NT) {
+    __syncthreads();
+    const double ow = gt_apply(L, L.tv, L.rhs);
+    if (threadIdx.x == 0) L.rhs[L.N] = ow;
+    __syncthreads();
+    for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
+    __syncthreads();
+}
+PHASE void ph_newton_back(Ctx c, int corr, double smu) {
+    LAYDEF;
+    g_apply(L, L.dz, L.ds, false);
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
+        const double dsr = -L.rp[r] - L.ds[r];
+        L.ds[r] = dsr;
+        L.dl[r] = -(rc + L.lam[r] * dsr) / L.s[r];
+    }
+    __syncthreads();
+}
+// predictor step length and Mehrotra centring: returns sigma * mu; stores the affine direction
+PHASE double ph_affine(Ctx c, double mu) {
+    LAYDEF;
+    const double aaff = max_step(L);
+    double mua = 0.0;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        mua += (L.s[r] + aaff * L.ds[r]) * (L.lam[r] + aaff * L.dl[r]);
+        L.sa[r] = L.ds[r];
+        L.la[r] = L.dl[r];
+    }
+    double red[4] = {mua, 0.0, 0.0, 0.0};
+    block_reduce4(red, 0, L.red);
+    const double sr = red[0] / L.mc / mu;
+    return sr * sr * sr * mu;
+}
+PHASE void ph_update(Ctx c) {
+    LAYDEF;
+    const double alpha = fmin(1.0, 0.99 * max_step(L));
+    for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] += alpha * L.dz[e];
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        L.s[r] += alpha * L.ds[r];
+        L.lam[r] += alpha * L.dl[r];
+    }
+    __syncthreads();
+}
+// polish: weights 1/delta on the active set {lam > s}, y = lam there, x_0 = z
+PHASE void ph_polish_prep(Ctx c) {
+    LAYDEF;
+    const double idl = 1.0 / P.polDelta;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
         const bool act = L.lam[r] > L.s[r];
         L.dd[r] = act ? idl : 0.0;
         L.la[r] = act ? L.lam[r] : 0.0;   // y
         L.sa[r] = act ? 1.0 : 0.0;        // active mask
     }
-    for (int e = tid; e < n; e += NT) L.dz[e] = L.z[e];
+    for (int e = threadIdx.x; e < L.n; e += NT) L.dz[e] = L.z[e];
     __syncthreads();
+}
+PHASE void ph_polish_tv(Ctx c) {
+    LAYDEF;
+    const double idl = 1.0 / P.polDelta;
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
+    __syncthreads();
+}
+// rp = G x_k - h;  y += rp / delta on the active set
+PHASE void ph_polish_dual(Ctx c) {
+    LAYDEF;
+    const double idl = 1.0 / P.polDelta;
+    g_apply(L, L.dz, L.rp, true);
+    for (int r = threadIdx.x; r < L.mc; r += NT)
+        if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
+    __syncthreads();
+}
+// certify the polished point (primal feasible, y >= 0, finite); accept -> z
+PHASE int ph_polish_accept(Ctx c, double hmax) {
+    LAYDEF;
+    const int tid = threadIdx.x;
+    double viol = -1e300, ymin = 1e300, ymax = 0.0, nonfin = 0.0;
+    for (int r = tid; r < L.mc; r += NT) {
+        viol = fmax(viol, L.rp[r]);
+        if (L.sa[r] != 0.0) {
+            ymin = fmin(ymin, L.la[r]);
+            ymax = fmax(ymax, fabs(L.la[r]));
+        }
+    }
+    for (int e = tid; e < L.n; e += NT)
+        if (!isfinite(L.dz[e])) nonfin = 1.0;
+    double red[4] = {viol, -ymin, ymax, nonfin};
+    block_reduce4(red, 15, L.red);
+    const bool ok = red[0] <= 1e-9 * hmax && -red[1] >= -1e-9 * fmax(1.0, red[2]) && red[3] == 0.0;
+    if (ok)
+        for (int e = tid; e < L.n; e += NT) L.z[e] = L.dz[e];
+    __syncthreads();
+    return ok ? 1 : 0;
+}
+// u-bar <- uLim * z  (unscaled controls of the QP solution)
+PHASE void ph_take_u(Ctx c) {
+    LAYDEF;
+    for (int i = threadIdx.x; i < L.N; i += NT) L.ub[i] = P.uLim * L.z[i];
+    __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
+// variables, x = z = [u~ (N), omega]).  Returns IPM iterations; sets *qflags.
+// ---------------------------------------------------------------------------
+template <bool HG, bool VG, int RM>
+__device__ __noinline__ int qp_solve(Ctx c, int* qflags) {
+    const DevParams& P = *c.P;
+    const int mc = (P.nV * (P.nV - 1) / 2 + P.nV * P.nO) * c.Hb + 2 * P.nV * c.Hb + 1;
+    // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
+    const D4 sc = PH(ph_init_a)(c);
+    const double hmax = sc.a, qmax = sc.b;
+    PH(ph_assemble)(c, 0.0);
+    PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
+    PH(ph_rhs_from_tv)(c, 0.0);
+    PH(ph_solve)(c, 0);
+    PH(ph_init_b)(c);
+    // ---- Mehrotra iterations
+    int it = 0;
+    bool conv = false;
+    PROF_T0();
+    for (; it < P.maxIpm; ++it) {
+        PROF_ACC(0);
+        const D4 res = PH(ph_residuals)(c);
+        PROF_ACC(1);
+        if (res.a <= P.ipmTol * hmax && res.b <= P.ipmTol * qmax &&
+            res.c <= P.ipmTol * fmax(1.0, fabs(res.d))) {
+            conv = true;
+            break;
+        }
+        const double mu = res.c / mc;
+        PH(ph_scaling)(c);
+        PH(ph_assemble)(c, 0.0);
+        PROF_ACC(2);
+        if (!PH(ph_cholesky)(c)) break;
+        PROF_ACC(3);
+        PH(ph_newton_rhs)(c, 0, 0.0);
+        PROF_ACC(4);
+        PH(ph_solve)(c, 1);
+        PROF_ACC(9);
+        PH(ph_newton_back)(c, 0, 0.0);
+        const double smu = PH(ph_affine)(c, mu);
+        PH(ph_newton_rhs)(c, 1, smu);
+        PROF_ACC(5);
+        PH(ph_solve)(c, 1);
+        PROF_ACC(9);
+        PH(ph_newton_back)(c, 1, smu);
+        PH(ph_update)(c);
+        PROF_ACC(6);
+    }
+    if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
+    // ---- active-set polish: proximal method of multipliers on {lam > s}
+    PH(ph_polish_prep)(c);
 #ifdef SCPQP_PROF
     _pt = __builtin_amdgcn_s_memtime();
 #endif
-    assemble(P, L, L.dd, rho);
-    bool ok = cholesky(L);
+    PH(ph_assemble)(c, P.polRho);
+    const bool fact = PH(ph_cholesky)(c) != 0;
     PROF_ACC(7);
-    if (ok) {
+    bool ok = false;
+    if (fact) {
         for (int ref = 0; ref < P.nRefine; ++ref) {
-            for (int r = tid; r < mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
-            __syncthreads();
-            const double ow = gt_apply(L, L.tv, L.rhs);
-            if (tid == 0) L.rhs[N] = ow - P.slackW + rho * L.dz[N];
-            __syncthreads();
-            for (int e = tid; e < N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
-            __syncthreads();
-            chol_solve(L, L.rhs, L.dz);
-            g_apply(L, L.dz, L.rp, true);   // rp = G x - h
-            for (int r = tid; r < mc; r += NT)
-                if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
-            __syncthreads();
+            PH(ph_polish_tv)(c);
+            PH(ph_rhs_from_tv)(c, P.polRho);
+            PH(ph_solve)(c, 1);
+            PH(ph_polish_dual)(c);
         }
-        double viol = -1e300, ymin = 1e300, ymax = 0.0, nonfin = 0.0;
-        for (int r = tid; r < mc; r += NT) {
-            viol = fmax(viol, L.rp[r]);
-            if (L.sa[r] != 0.0) {
-                ymin = fmin(ymin, L.la[r]);
-                ymax = fmax(ymax, fabs(L.la[r]));
-            }
-        }
-        for (int e = tid; e < n; e += NT)
-            if (!isfinite(L.dz[e])) nonfin = 1.0;
-        double red[4] = {viol, -ymin, ymax, nonfin};
-        block_reduce4(red, 15, L.red);
-        ok = red[0] <= 1e-9 * hmax && -red[1] >= -1e-9 * fmax(1.0, red[2]) && red[3] == 0.0;
+        ok = PH(ph_polish_accept)(c, hmax) != 0;
     }
     PROF_ACC(8);
-    if (ok) {
-        for (int e = tid; e < n; e += NT) L.z[e] = L.dz[e];
-    } else {
-        *qflags |= SCPQP_FL_POLISH_REJECTED;
-    }
-    __syncthreads();
+    if (!ok) *qflags |= SCPQP_FL_POLISH_REJECTED;
     return it;
 }
 
@@ -1453,13 +1600,19 @@ __device__ int qp_solve(const DevParams& P, const LT& L, int* qflags) {
 // Kernel
 // ---------------------------------------------------------------------------
 template <bool HG, bool VG, int RM>
-__global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
+__global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
     ldouble* smem = (ldouble*)smem_;
     const DevParams& P = *a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
     const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
-    lint* slot = (lint*)(smem + f.red + 60);
+    lint* slot = (lint*)(smem + f.red + 124);
+    ldouble* lub = smem + f.ub;   // u-bar
+    ldouble* lpb = smem + f.pb;   // positions of the last evaluated u
+    ldouble* lref = smem + f.ref;
+    ldouble* lg = smem + f.g;
+    ldouble* lp0 = smem + f.p0;
+    ldouble* lqs = smem + f.qs;
     for (;;) {
         if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
         __syncthreads();
@@ -1467,8 +1620,8 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
         __syncthreads();
         if (b >= a.B) break;
         const int Hb = a.hp ? a.hp[b] : P.hpMax;
-        const Lay<HG, VG, RM> L = make_lay<HG, VG, RM>(smem, ws, f, P.nV, P.nO, Hb);
-        const int V = L.V, N = L.N;
+        const Ctx c{a.P, ws, Hb};
+        const int V = P.nV, N = V * Hb, O = P.nO;
         PROF_T0();
         const int sflag = setup_problem_ni<HG, VG, RM>(a, ws, b, Hb);
         PROF_ACC(10);
@@ -1476,36 +1629,36 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
         if (a.mode == MODE_SAMPLE) {
             for (int i = tid; i < Hb * 2 * V; i += NT) {
-                const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
-                a.refOut[(size_t)b * P.hpMax * 2 * V + i] = L.ref[(v * Hb + k) * 2 + c];
+                const int k = i / (2 * V), cc = (i / V) & 1, v = i % V;
+                a.refOut[(size_t)b * P.hpMax * 2 * V + i] = lref[(v * Hb + k) * 2 + cc];
             }
             continue;
         }
         if (a.mode == MODE_LINEARIZE) {
             for (int i = tid; i < V * Hb * 2; i += NT) {
-                if (a.gOut) a.gOut[slotU * 2 + i] = L.g[i];
-                if (a.p0Out) a.p0Out[slotU * 2 + i] = L.p0[i];
+                if (a.gOut) a.gOut[slotU * 2 + i] = lg[i];
+                if (a.p0Out) a.p0Out[slotU * 2 + i] = lp0[i];
             }
             for (int i = tid; i < N; i += NT)
-                if (a.psiOut) a.psiOut[slotU + i] = L.qs[i] / P.uLim;
+                if (a.psiOut) a.psiOut[slotU + i] = lqs[i] / P.uLim;
             if (a.refOut)
                 for (int i = tid; i < Hb * 2 * V; i += NT) {
-                    const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
-                    a.refOut[(size_t)b * P.hpMax * 2 * V + i] = L.ref[(v * Hb + k) * 2 + c];
+                    const int k = i / (2 * V), cc = (i / V) & 1, v = i % V;
+                    a.refOut[(size_t)b * P.hpMax * 2 * V + i] = lref[(v * Hb + k) * 2 + cc];
                 }
             __syncthreads();
             continue;
         }
         if (a.mode == MODE_EVALUATE) {
-            for (int i = tid; i < N; i += NT) L.ub[i] = a.uEval[slotU + i];
+            for (int i = tid; i < N; i += NT) lub[i] = a.uEval[slotU + i];
             double* cv = a.cveh ? a.cveh + (size_t)b * V * V * P.hpMax : nullptr;
-            double* co = a.cobs ? a.cobs + (size_t)b * V * L.O * P.hpMax : nullptr;
+            double* co = a.cobs ? a.cobs + (size_t)b * V * O * P.hpMax : nullptr;
             if (cv)
                 for (int i = tid; i < V * V * Hb; i += NT) cv[i] = -INFINITY;
             if (co)
-                for (int i = tid; i < V * L.O * Hb; i += NT) co[i] = -INFINITY;
+                for (int i = tid; i < V * O * Hb; i += NT) co[i] = -INFINITY;
             __syncthreads();
-            const EvalRes ev = evaluate_u(P, L, L.ub, cv, co);
+            const EvalRes ev = PH(ph_evaluate)(c, cv, co);
             if (tid == 0) {
                 if (a.obj) a.obj[b] = ev.obj;
                 if (a.maxv) a.maxv[b] = ev.maxv;
@@ -1514,29 +1667,30 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
             }
             if (a.trajOut)
                 for (int i = tid; i < Hb * 2 * V; i += NT) {
-                    const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
-                    a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = L.pb[(v * Hb + k) * 2 + c];
+                    const int k = i / (2 * V), cc = (i / V) & 1, v = i % V;
+                    a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = lpb[(v * Hb + k) * 2 + cc];
                 }
             __syncthreads();
             continue;
         }
         // ------------------------------- SCP solve (SCP_controller.py:40-197)
-        for (int i = tid; i < N; i += NT) L.ub[i] = a.uWarm ? a.uWarm[slotU + i] : 0.0;
+        for (int i = tid; i < N; i += NT) lub[i] = a.uWarm ? a.uWarm[slotU + i] : 0.0;
         __syncthreads();
-        if (tid == 0 && fabs(L.ub[0]) < 2.220446049250313e-16) L.ub[0] = 2.220446049250313e-16;
+        if (tid == 0 && fabs(lub[0]) < 2.220446049250313e-16) lub[0] = 2.220446049250313e-16;
         __syncthreads();
-        EvalRes ev = evaluate_u(P, L, L.ub, nullptr, nullptr);
+        EvalRes ev = PH(ph_evaluate)(c, nullptr, nullptr);
         double obj0 = ev.obj, mv0 = ev.maxv;
         const int maxScp = a.maxScp > 0 ? a.maxScp : P.maxScp;
         int qflags = 0, nipm = 0, it = 0, status = SCPQP_ST_MAX_SCP;
         for (it = 0; it < maxScp; ++it) {
-            PROF_T0();
-            linearise_rows(P, L);
+#ifdef SCPQP_PROF
+            _pt = __builtin_amdgcn_s_memtime();
+#endif
+            PH(ph_linearise)(c);
             PROF_ACC(11);
-            nipm += qp_solve(P, L, &qflags);
-            for (int i = tid; i < N; i += NT) L.ub[i] = P.uLim * L.z[i];
-            __syncthreads();
-            ev = evaluate_u(P, L, L.ub, nullptr, nullptr);
+            nipm += qp_solve<HG, VG, RM>(c, &qflags);
+            PH(ph_take_u)(c);
+            ev = PH(ph_evaluate)(c, nullptr, nullptr);
             const double delta = (obj0 + P.slackW * mv0) - (ev.obj + P.slackW * ev.maxv);
             obj0 = ev.obj;
             mv0 = ev.maxv;
@@ -1555,13 +1709,13 @@ __global__ __launch_bounds__(NT) void scp_kernel(KArgs a) {
         }
         const int nscp = it < maxScp ? it + 1 : maxScp;
         if (V == 1 && !ev.feasible && status != SCPQP_ST_NUMERIC) status = SCPQP_ST_INVALID;
-        // outputs (positions of the final u are in L.pb from the last evaluate)
+        // outputs (positions of the final u are in pb from the last evaluate)
         if (a.uOut)
-            for (int i = tid; i < N; i += NT) a.uOut[slotU + i] = L.ub[i];
+            for (int i = tid; i < N; i += NT) a.uOut[slotU + i] = lub[i];
         if (a.trajOut)
             for (int i = tid; i < Hb * 2 * V; i += NT) {
-                const int k = i / (2 * V), c = (i / V) & 1, v = i % V;
-                a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = L.pb[(v * Hb + k) * 2 + c];
+                const int k = i / (2 * V), cc = (i / V) & 1, v = i % V;
+                a.trajOut[(size_t)b * P.hpMax * 2 * V + i] = lpb[(v * Hb + k) * 2 + cc];
             }
         if (tid == 0) {
             if (a.status) a.status[b] = status | qflags | (sflag_any ? SCPQP_FL_SAMPLER : 0);
