@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""Benchmark: batched SCP-QP solves/sec on MI355X (BASELINE.json metric).
+
+One *step* = one full SCP solve (linearise dynamics, then the <=20 convexified
+QPs under the reference's stopping rule, SCP_controller.py:40-197) of every
+problem of a batch of synthetic problems, in ONE kernel launch.  Workload at
+N=1 is BASELINE config c2: the 4-vehicle circle ("crossing") scenario,
+Hp = 20, batch = 1024 noise seeds.  With N GPUs each rank solves its own 1024
+problems (global problem indices rank*1024 ...), no collective on the data
+path ("weak" scaling); only a barrier and a max-reduction of the time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+
+Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant (only)
+kernel against the FP64 peak with the algorithmic FLOP count of the executed
+algorithm (scpqp/flops.py); ``cpu_baseline`` times the in-repo CPU
+restatement of the reference path (oracle/, faithful mode) on a bounded sample
+of the same problems on the host cores, and ``traj_linf_err`` is the GPU-vs-
+oracle trajectory error on that sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+
+FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD datasheet
+HBM_PEAK_GBS = 8000.0
+METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    """Spawned worker: the oracle's faithful restatement of the reference path."""
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    sys.path.insert(0, ROOT)
+    from oracle import scp_reference as R
+    n_veh, hp, x0s, u0s, ecs = args
+    sc = R.circle_scenario(n_veh, Hp=hp)
+    out = []
+    t0 = time.perf_counter()
+    for x0, u0, ec in zip(x0s, u0s, ecs):
+        p = R.make_problem(sc, x0, u0, ec, Hp=hp)
+        r = R.scp_solve(p, mode="faithful")
+        out.append((r.traj, r.n_scp))
+    return time.perf_counter() - t0, out
+
+
+def cpu_baseline(bt, n_veh, hp, sample, workers):
+    idx = np.arange(sample)
+    chunks = [c for c in np.array_split(idx, workers) if len(c)]
+    jobs = [(n_veh, hp, bt.x0[c], bt.u0[c], bt.ec_noise[c]) for c in chunks]
+    ctx = mp.get_context("spawn")
+    env_keep = os.environ.get("OMP_NUM_THREADS")
+    os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    t0 = time.perf_counter()
+    with ctx.Pool(len(jobs)) as pool:
+        res = pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    if env_keep is not None:
+        os.environ["OMP_NUM_THREADS"] = env_keep
+    cpu_s = sum(r[0] for r in res)
+    trajs = [t for r in res for t in r[1]]
+    return wall, cpu_s, trajs
+
+
+def host_cores():
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    # the GPU box exposes the whole machine's CPUs; its share is 16 (gpurun docs)
+    return max(1, min(n, int(os.environ.get("SCPQP_CPU_WORKERS", "16"))))
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (config c2: 1024)")
+    ap.add_argument("--n-veh", type=int, default=4)
+    ap.add_argument("--hp", type=int, default=20)
+    ap.add_argument("--cpu-sample", type=int, default=128)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
+
+    from scpqp import flops as FL
+    from scpqp import shard
+    import Scenarios  # the drop-in scenario module (host logic)
+
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = args.hp
+    sc.get_circle_scenario([2 * math.pi / args.n_veh * (i + 1) for i in range(args.n_veh)])
+    sc.complete_scenario()
+    B = args.batch
+    bt = shard.shard_batch(sc, B, rank, base_seed=0)
+
+    # CPU baseline first (rank 0, N=1): spawned workers, before this process touches the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cores = host_cores()
+        sample = min(args.cpu_sample, B)
+        wall, cpu_s, cpu_trajs = cpu_baseline(bt, args.n_veh, args.hp, sample, cores)
+        cpu = dict(wall=wall, cpu_s=cpu_s, trajs=cpu_trajs, cores=cores, sample=sample)
+
+    import torch
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        dist = None
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    from scpqp.solver import ScpQpSolver
+
+    S = ScpQpSolver(sc, max_batch=B, device=dev)
+    x0 = torch.as_tensor(bt.x0, device=dev)
+    u0 = torch.as_tensor(bt.u0, device=dev)
+    ec = torch.as_tensor(bt.ec_noise, device=dev)
+    out = S.alloc_out(B)
+    stream = torch.cuda.current_stream(dev)
+
+    for _ in range(args.warmup):
+        S.solve(x0, u0, ec, out=out)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        S.solve(x0, u0, ec, out=out)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)   # one launch per step
+    elapsed = shard.max_over_ranks(elapsed, dist, dev)
+
+    n_scp = out.n_scp.cpu().numpy()
+    n_ipm = out.n_ipm.cpu().numpy()
+    status = out.status.cpu().numpy()
+    flops = FL.batch_flops(args.n_veh, bt.hp, 0, n_scp, n_ipm, 10)
+    achieved_tf = flops / (kern_ms * 1e-3) / 1e12
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+
+    traffic = None
+    if os.path.exists(PMC_SUMMARY):
+        try:
+            with open(PMC_SUMMARY) as fh:
+                traffic = json.load(fh).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    line = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "SCP solves/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (circle scenario x0 + N(0,diag(.05,.05,.005,.02,0,.002)^2), Ec noise N(0,3e-6^2))",
+        "config": {"workload": f"c2: {args.n_veh}-vehicle circle/crossing, Hp={args.hp}, "
+                               f"batch={B} noise seeds per GPU, full SCP solve per problem",
+                   "n_veh": args.n_veh, "hp": args.hp, "batch_per_gpu": B,
+                   "parallelism": f"{world} independent shards (no collective)"},
+        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "scp_kernel", "kernel_ms": kern_ms,
+                     "flops_per_launch": flops,
+                     "peak_note": "FP64 dense peak (vector = MFMA rate on gfx950, AMD spec)"},
+        "qp_solves_per_s": world * float(n_scp.sum()) * args.steps / elapsed,
+        "mean_scp_iters": float(n_scp.mean()),
+        "mean_ipm_iters_per_qp": float(n_ipm.sum() / max(n_scp.sum(), 1)),
+        "status_converged_frac": float(np.mean((status & 0xff) == 0)),
+    }
+    if cpu is not None:
+        trajs = out.traj.cpu().numpy()
+        errs = []
+        for b, (tr, ns) in enumerate(cpu["trajs"]):
+            if ns == n_scp[b]:
+                errs.append(float(np.abs(trajs[b] - tr).max()))
+        line["cpu_baseline"] = {
+            "value": cpu["sample"] / cpu["wall"], "unit": "SCP solves/s", "cores": cpu["cores"],
+            "kind": "port",
+            "sample": f"first {cpu['sample']} problems of the same c2 batch, oracle faithful mode "
+                      f"(dense QCQP_formulate tensors, scipy expm, dense IPM + exact polish), "
+                      f"{cpu['cores']} spawned single-threaded workers; "
+                      f"{cpu['cpu_s']:.1f} s of CPU work",
+        }
+        line["traj_linf_err"] = max(errs) if errs else None
+        line["traj_err_sample"] = f"{len(errs)}/{cpu['sample']} problems with equal SCP iteration count"
+    if rank == 0:
+        print(json.dumps(line))
+    if dist:
+        dist.destroy_process_group()
+    S.close()
+
+
+if __name__ == "__main__":
+    main()

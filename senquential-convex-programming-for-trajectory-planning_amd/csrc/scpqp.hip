@@ -1620,6 +1620,14 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
         __syncthreads();
         if (b >= a.B) break;
         const int Hb = a.hp ? a.hp[b] : P.hpMax;
+        if (Hb < 1 || Hb > P.hpMax) {   // horizon outside the slot: report, never index with it
+            if (tid == 0) {
+                if (a.status) a.status[b] = SCPQP_ST_INVALID;
+                if (a.nscp) a.nscp[b] = 0;
+                if (a.nipm) a.nipm[b] = 0;
+            }
+            continue;
+        }
         const Ctx c{a.P, ws, Hb};
         const int V = P.nV, N = V * Hb, O = P.nO;
         PROF_T0();

@@ -19,7 +19,8 @@ array          shape                   meaning (reference field)
 ``ec_noise``   [B, nVeh, 2]            the two N(0, 3e-6) draws Model.py:85-86
                                        adds to dx[0], dx[1] inside comp_jacobian
 ``hp``         [B] int32               per-problem horizon (mixed-horizon c5)
-``obst``       [B, nObst, 2, Hp_max]   Iter.obstacleFutureTrajectories
+``obst``       [B, nObst, 2, Hp_max]   Iter.obstacleFutureTrajectories; each
+                                       slot holds [nObst][2][hp_b] packed
 =============  ======================  =========================================
 """
 from __future__ import annotations
@@ -109,8 +110,12 @@ def make_batch(scenario, B, base_seed=0, offset=0, perturb=True, noise=True, hp=
             if noise:
                 ec[b] = en
     u0 = np.zeros((B, nV))
+    # per-problem slot of nObst*2*hp_max doubles holding [nObst][2][hp_b] packed
+    # (include/scpqp.h: per-problem arrays use their own horizon inside the slot)
     obst = np.zeros((B, nO, 2, hp_max))
     if nO:
-        base = obstacle_prediction(scenario, hp_max)
-        obst[:] = base[None]
+        flat = obst.reshape(B, -1)
+        for H in np.unique(hps):
+            base = obstacle_prediction(scenario, int(H)).reshape(-1)
+            flat[hps == H, :base.size] = base
     return Batch(np.ascontiguousarray(x0), u0, ec, hps, obst, hp_max, seeds)

@@ -1,0 +1,102 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly
+what include/scpqp.h declares, the ctypes structures match the C layout
+(checked with a gcc-compiled probe of the header), and argument validation
+returns the documented error codes without touching a device."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import pytest
+
+from scpqp import _lib as LB
+from scpqp.build import LIB_PATH
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "scpqp.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(scpqp_\w+)\(", txt, re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB_PATH):
+        pytest.fail("libscpqp.so not built: run __graft_entry__.build()")
+    return LB.load()
+
+
+def test_header_declares_the_boundary():
+    fns = header_functions()
+    assert fns == sorted(["scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version",
+                          "scpqp_solve", "scpqp_linearize", "scpqp_evaluate",
+                          "scpqp_sample_reference", "scpqp_resources"])
+    assert sorted(LB.EXPORTS) == fns
+
+
+def test_library_exports_every_declared_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\sT\s(scpqp_\w+)", out))
+    assert set(header_functions()) <= exported
+    for name in header_functions():
+        assert hasattr(lib, name)
+
+
+def test_version_and_error_strings(lib):
+    v = lib.scpqp_version().decode()
+    assert "scpqp" in v and "gfx950" in v
+    assert isinstance(lib.scpqp_last_error(), bytes)
+
+
+def test_argument_validation_without_gpu(lib):
+    h = C.c_void_p()
+    assert lib.scpqp_create(None, None, 0, C.byref(h)) == -1
+    assert b"null" in lib.scpqp_last_error()
+    D = LB.Dims(n_veh=0, hp_max=10, n_obst=0, max_batch=1)
+    P = LB.Params()
+    assert lib.scpqp_create(C.byref(D), C.byref(P), 0, C.byref(h)) == -1
+    D = LB.Dims(n_veh=17, hp_max=10, n_obst=0, max_batch=1)
+    assert lib.scpqp_create(C.byref(D), C.byref(P), 0, C.byref(h)) == -1
+    D = LB.Dims(n_veh=8, hp_max=64, n_obst=0, max_batch=1)
+    assert lib.scpqp_create(C.byref(D), C.byref(P), 0, C.byref(h)) == -4   # n > 256: SCPQP_E_SIZE
+    D = LB.Dims(n_veh=4, hp_max=20, n_obst=0, max_batch=1)
+    assert lib.scpqp_create(C.byref(D), C.byref(P), 0, C.byref(h)) == -1   # null per-vehicle params
+    assert lib.scpqp_destroy(None) == 0
+    bi = LB.BatchIn()
+    bo = LB.BatchOut()
+    assert lib.scpqp_solve(None, 1, C.byref(bi), C.byref(bo), None) == -1
+
+
+PROBE = r"""
+#include <stddef.h>
+#include <stdio.h>
+#include "scpqp.h"
+#define S(t) printf(#t " %zu\n", sizeof(t));
+#define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f));
+int main(void) {
+  S(scpqp_dims) S(scpqp_params) S(scpqp_batch_in) S(scpqp_batch_out) S(scpqp_lin_out) S(scpqp_eval_out)
+  %s
+  return 0;
+}
+"""
+
+
+def test_ctypes_layout_matches_header(tmp_path):
+    structs = {"scpqp_dims": LB.Dims, "scpqp_params": LB.Params, "scpqp_batch_in": LB.BatchIn,
+               "scpqp_batch_out": LB.BatchOut, "scpqp_lin_out": LB.LinOut,
+               "scpqp_eval_out": LB.EvalOut}
+    offs = "".join(f"O({cn}, {f}) " for cn, cls in structs.items() for f, _ in cls._fields_)
+    src = tmp_path / "probe.c"
+    src.write_text(PROBE.replace("%s", offs))
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", f"-I{os.path.dirname(HEADER)}", str(src), "-o", str(exe)],
+                   check=True)
+    got = dict(line.rsplit(" ", 1) for line in subprocess.run(
+        [str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for cn, cls in structs.items():
+        assert int(got[cn]) == C.sizeof(cls), cn
+        for f, _ in cls._fields_:
+            assert int(got[f"{cn}.{f}"]) == getattr(cls, f).offset, f"{cn}.{f}"

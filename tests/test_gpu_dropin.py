@@ -1,0 +1,189 @@
+"""The drop-in modules driven the way the reference's main.py drives them
+(main.py:98-206): IterClass -> SCPcontroller(scenario, Iter, prevOutput) ->
+SCP_controller -> steering clip -> plant step -> QCQP_evaluate /
+evaluateInOriginalProblem, for a few MPC steps.  Every step's controller
+output is checked against the CPU restatement on the same Iter inputs and
+warm start.
+"""
+import math
+
+import numpy as np
+import pytest
+import scipy.integrate
+
+import MPC_Iter
+import SampleReferTraj
+import Scenarios
+from oracle import scp_reference as R
+from SCP_controller import SCPcontroller
+
+pytestmark = pytest.mark.gpu
+
+
+def oracle_for(sc):
+    o = R.OracleScenario(Hp=sc.Hp, Hu=sc.Hu, dsafeExtra=sc.dsafeExtra)
+    for v in range(sc.nVeh):
+        x = np.asarray(sc.x0[v]).reshape(-1)
+        o.add_vehicle(x[0], x[1], x[2], sc.referenceTrajectories[v])
+    o.obstacles = [np.asarray(ob, float).reshape(-1) for ob in sc.obstacles]
+    return o.complete()
+
+
+def run_loop(sc, steps):
+    """A condensed main.py loop (main.py:98-192) over the drop-in modules."""
+    nV, nx = sc.nVeh, sc.model.nx
+    tps, tdu = sc.ticks_per_sim, sc.ticks_delay_u
+    ticks = sc.ticks_total
+    path = np.full((nx, nV, ticks + 1), np.nan)
+    ctrl = np.full((nV, ticks + 1), np.nan)
+    for v in range(nV):
+        path[:, v, 0] = np.asarray(sc.x0[v]).reshape(-1)
+        ctrl[v, 0:tdu + tps + 1] = sc.u0[v]
+    obst_path = None
+    if sc.nObst:
+        obs = np.asarray(sc.obstacles, float).reshape(sc.nObst, 6)
+        t = np.arange(ticks + 1) * sc.tick_length
+        obst_path = np.zeros((sc.nObst, 2, ticks + 1))
+        obst_path[:, 0] = obs[:, 0:1] + t[None] * (obs[:, 3] * np.cos(obs[:, 2]))[:, None]
+        obst_path[:, 1] = obs[:, 1:2] + t[None] * (obs[:, 3] * np.sin(obs[:, 2]))[:, None]
+    outputs, records = [], []
+    for i in range(steps):
+        now = i * tps
+        act = min(ticks + 1, now + 1 + tdu + tps)
+        u_path = np.zeros((nV, tps + tdu))
+        u_path[:, :act - 1 - now] = ctrl[:, now + 1:act]
+        uMax = np.full((1, nV), sc.mechanicalSteeringLimit)
+        obst_state = obst_path[:, :, now] if sc.nObst else np.zeros((0, 2))
+        it = MPC_Iter.IterClass(sc, path[:, :, now].T, u_path, obst_state, uMax)
+        prev = outputs[i - 1] if i else outputs
+        warm = None if i == 0 else np.array(prev['u'], float).reshape(-1)
+        c = SCPcontroller(sc, it, prev)
+        U, traj, out = c.SCP_controller(it)
+        outputs.append(out)
+        records.append(dict(Iter=it, U=np.array(U, float).reshape(sc.Hp, nV), traj=traj, out=out,
+                            warm=warm, ctrl=c))
+        U = np.array(U, float).reshape(sc.Hp, nV)
+        for v in range(nV):
+            U[0, v] = np.clip(U[0, v], -uMax[0, v], uMax[0, v])
+            lo = now + 1 + tdu + tps
+            ctrl[v, lo:min(lo + tps, ticks + 1)] = U[0, v]
+            f = lambda t, x: sc.model.odes_(t, x, ctrl[v, min(ticks, math.ceil(t / sc.tick_length) + 1)],
+                                            sc.Lf[v], sc.Lr[v])           # noqa: E731
+            sol = scipy.integrate.solve_ivp(f, (i * sc.dt, (i + 1) * sc.dt), path[:, v, now],
+                                            t_eval=np.linspace(i * sc.dt, (i + 1) * sc.dt, tps + 1),
+                                            rtol=1e-8, atol=1e-8)
+            path[:, v, now + 1:now + tps + 1] = sol.y[:, 1:]
+    return records
+
+
+def check_against_oracle(sc, rec):
+    o = oracle_for(sc)
+    it = rec["Iter"]
+    obst = it.obstacleFutureTrajectories if sc.nObst else None
+    p = R.make_problem(o, it.x0, it.u0.reshape(-1), None, Hp=sc.Hp, obst=obst,
+                       ref_points=it.ReferenceTrajectoryPoints)
+    # the device sampler against the restatement on the same delay-compensated state
+    want_ref = R.reference_points(o, it.x0, sc.Hp)
+    assert np.max(np.abs(it.ReferenceTrajectoryPoints - want_ref)) <= 1e-12
+    r = R.scp_solve(p, u_warm=rec["warm"], mode="structured")
+    log = rec["out"]["optimization_log"]
+    if log["n_scp"] == r.n_scp:
+        assert np.max(np.abs(rec["out"]["u"].reshape(-1) - r.u)) <= 1e-7
+        assert np.max(np.abs(rec["traj"] - r.traj)) <= 1e-6
+    return log["n_scp"] == r.n_scp
+
+
+def test_circle4_closed_loop():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 20
+    sc.get_circle_scenario([2 * math.pi / 4 * (i + 1) for i in range(4)])
+    sc.complete_scenario()
+    recs = run_loop(sc, 3)
+    agree = [check_against_oracle(sc, r) for r in recs]
+    assert sum(agree) >= 2
+    r0 = recs[0]
+    assert r0["U"].shape == (20, 4) and r0["traj"].shape == (20, 2, 4)
+    assert r0["out"]["u"].shape == (80, 1) and r0["out"]["resultInvalid"] is False
+    # QCQP_evaluate at zero input (main.py:197) and evaluateInOriginalProblem (main.py:201)
+    c = r0["ctrl"]
+    res = c.QCQP_evaluate(np.zeros((80, 1)))
+    assert len(res) == 8 and res[1].shape == (1, 1) and res[6].shape == (4, 4, 20)
+    o = oracle_for(sc)
+    it = r0["Iter"]
+    p = R.make_problem(o, it.x0, it.u0.reshape(-1), None, Hp=20,
+                       ref_points=it.ReferenceTrajectoryPoints)
+    L = R.linearise(p, "faithful")
+    q = R.qcqp_formulate(p, L)
+    ev = R.qcqp_evaluate_dense(q, np.zeros(80), 4, 20, 0)
+    assert res[0] == ev.feasible
+    assert res[1][0, 0] == pytest.approx(ev.obj, rel=1e-10)
+    fin = np.isfinite(ev.c_veh)
+    assert np.allclose(res[6][fin], ev.c_veh[fin], rtol=0, atol=1e-9)
+    assert np.array_equal(np.isfinite(res[6]), fin)
+    e = c.evaluateInOriginalProblem(r0["U"], r0["traj"], {'ignoreQCQPcheck': True})
+    assert e['predictionObjectiveValue'] == pytest.approx(
+        R.evaluate_structured(p, L, r0["out"]["u"].reshape(-1)).obj, rel=1e-9)
+
+
+def test_mpcclass_matches_restatement():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 12
+    sc.get_circle_scenario([2 * math.pi / 3 * (i + 1) for i in range(3)])
+    sc.complete_scenario()
+    recs = run_loop(sc, 1)
+    c = recs[0]["ctrl"]
+    it = recs[0]["Iter"]
+    o = oracle_for(sc)
+    p = R.make_problem(o, it.x0, it.u0.reshape(-1), None, Hp=12,
+                       ref_points=it.ReferenceTrajectoryPoints)
+    L = R.linearise(p, "faithful")
+    m = c.mpc
+    for v in range(3):
+        assert np.allclose(m.Mathcal_B[:, :, v], L.calB[v], rtol=1e-12, atol=1e-14)
+        assert np.allclose(m.const_term[:, 0, v], L.const[v], rtol=1e-12, atol=1e-12)
+        assert np.allclose(m.Phi_0[:, :, v], L.Phi0[v], rtol=1e-11)
+        assert np.allclose(m.Psi_0[:, 0, v], L.Psi0[v], rtol=1e-10, atol=1e-8)
+        assert m.gamma_0[0, v] == pytest.approx(L.gamma0[v], rel=1e-10)
+        cA, cC, _ = R.prediction_matrices(L.Ad[v], L.Bd[v][:, None], np.eye(2, 6), L.Ed[v][:, None],
+                                          12, 12)
+        assert np.allclose(m.Mathcal_A[:, :, v], cA, rtol=1e-11, atol=1e-13)
+        assert np.allclose(m.Mathcal_C[:, :, v], cC, rtol=1e-11, atol=1e-13)
+        assert np.allclose(m.A[:, :, 5, v], L.Ad[v], rtol=1e-12)
+    # the lazily built dense QCQP tensors equal QCQP_formulate's
+    q = R.qcqp_formulate(p, L)
+    d = c.qcqp
+    assert np.allclose(d['Phi'], q.Phi, atol=1e-10)
+    assert np.allclose(d['Psi'][..., 0], q.Psi, atol=1e-8)
+    assert np.allclose(d['gamma'], q.gamma, rtol=1e-10, atol=1e-8)
+
+
+def test_frog_single_vehicle_with_obstacles():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 10
+    sc.get_frog_scenario()
+    sc.complete_scenario()
+    recs = run_loop(sc, 2)
+    agree = [check_against_oracle(sc, r) for r in recs]
+    assert all(agree)
+    assert recs[0]["U"].shape == (10, 1)
+
+
+def test_eps_nudge_mutates_previous_output_in_place():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 10
+    sc.get_circle_scenario([math.pi, 2 * math.pi])
+    sc.complete_scenario()
+    recs = run_loop(sc, 1)
+    it = recs[0]["Iter"]
+    prev = {'u': np.zeros((20, 1))}
+    c = SCPcontroller(sc, it, prev)
+    c.SCP_controller(it)
+    assert prev['u'][0, 0] == np.spacing(1)          # SCP_controller.py:75-76 on a view (B.5)
+
+
+def test_sample_reference_free_function():
+    ref = np.array([[-30.0, 0.0], [30.0, 0.0]])
+    for (x, y, s, n) in [(-20.0, 0.3, 1.6, 10), (29.5, 0.0, 1.6, 6), (0.0, -2.0, 0.7, 64)]:
+        got = SampleReferTraj.sampleReferenceTrajectory(n, ref, x, y, s)
+        want = R.sample_reference(n, ref, x, y, s)
+        assert np.max(np.abs(got - want)) <= 1e-12

@@ -1,0 +1,180 @@
+"""Host-side logic of the drop-in modules and helpers, against the restatement.
+
+Only host code is exercised here (scenario builders, plant model, geometry
+helpers, delay compensation, obstacle prediction, batch generation, FLOP
+model); every solve/linearise/evaluate/sample call needs the GPU and lives in
+the -m gpu tests.
+"""
+import math
+
+import numpy as np
+import pytest
+
+import Config
+import MIQP
+import Model
+import MPC_Iter
+import SampleReferTraj
+import Scenarios
+from oracle import scp_reference as R
+from scpqp import batch as BT
+from scpqp import flops as FL
+
+
+def _circle(n, hp=10):
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = hp
+    sc.get_circle_scenario([2 * math.pi / n * (i + 1) for i in range(n)])
+    sc.complete_scenario()
+    return sc
+
+
+@pytest.mark.parametrize("kind", ["circle4", "circle8", "frog", "parallel5", "parallel11"])
+def test_scenarios_match_restatement(kind):
+    sc = Scenarios.Scenario(False)
+    if kind.startswith("circle"):
+        n = int(kind[6:])
+        sc.get_circle_scenario([2 * math.pi / n * (i + 1) for i in range(n)])
+        o = R.circle_scenario(n)
+    elif kind == "frog":
+        sc.get_frog_scenario()
+        o = R.frog_scenario()
+    else:
+        n = int(kind[8:])
+        sc.get_parallel_scenario(n)
+        sc.dsafeExtra = 0.9
+        o = R.parallel_scenario(n)
+    sc.complete_scenario()
+    assert sc.nVeh == o.nVeh and sc.nObst == o.nObst
+    assert np.array_equal(np.array(sc.x0).reshape(sc.nVeh, 6), np.array(o.x0))
+    assert np.array_equal(sc.dsafeVehicles, o.dsafeVehicles)
+    if sc.nObst:
+        assert np.array_equal(sc.dsafeObstacles, o.dsafeObstacles)
+        assert np.array_equal(np.asarray(sc.obstacles).reshape(sc.nObst, 6), np.array(o.obstacles))
+        assert np.asarray(sc.obstacles).shape == (sc.nObst, 6, 1)     # main.py:70 indexing
+    for a, b in zip(sc.referenceTrajectories, o.referenceTrajectories):
+        assert np.array_equal(np.asarray(a, float), b)
+    assert (sc.ticks_per_sim, sc.Nsim, sc.ticks_total, sc.ticks_delay_u) == (40, 50, 2000, 3)
+    assert sc.uLim == pytest.approx(math.pi / 60)
+    assert sc.dsafeExtra == o.dsafeExtra
+    if kind.startswith("circle"):
+        assert sc.CouplingAdjacencyMatrixPB.shape == (sc.nVeh, sc.nVeh)
+    elif kind.startswith("parallel"):
+        # Scenarios.py:197 builds np.diag(range(nVeh-1), 2): (nVeh+1) square, kept as is
+        assert sc.CouplingAdjacencyMatrixPB.shape == (sc.nVeh + 1, sc.nVeh + 1)
+
+
+def test_uLim_build_choice_and_override():
+    sc = _circle(2)
+    assert sc.uLim == sc.mechanicalSteeringLimit
+    sc.uLim = 0.1
+    assert sc.uLim == 0.1
+
+
+def test_model_matches_restatement():
+    m = Model.BicyleModel(False)
+    g = np.random.default_rng(2)
+    for _ in range(20):
+        x = np.array([*g.uniform(-5, 5, 2), g.uniform(-3, 3), g.uniform(1, 6), 0.0, g.uniform(-.2, .2)])
+        u = g.uniform(-0.05, 0.05)
+        assert np.array_equal(m.ode(x, 0.0, u, .34, .34), R.bicycle_rhs(x, u, .34, .34))
+        assert np.array_equal(m.odes_(0.0, x, u, .34, .34), R.bicycle_rhs(x, u, .34, .34))
+        a = m.comp_jacobian(x, np.array([u]), .34, .34)
+        b = R.bicycle_jacobian(x, u, .34, .34)
+        for p, q in zip(a, b):
+            assert np.array_equal(p, q)
+    veh = Model.DefaultVehicle()
+    m.makeInitState(veh)
+    assert m.makeInitStateVector.shape == (6, 1)
+    assert (veh.Q, veh.Q_final, veh.R, veh.Lf, veh.Lr) == (1, 20, 4000, .34, .34)
+
+
+def test_geometry_helpers_match_restatement():
+    g = np.random.default_rng(4)
+    for _ in range(50):
+        ref = g.uniform(-30, 30, (2, 2))
+        x, y = (float(v) for v in g.uniform(-30, 30, 2))
+        a = SampleReferTraj.getShortestDistance(ref[:, 0], ref[:, 1], x, y)
+        b = R.shortest_distance(ref[:, 0], ref[:, 1], x, y)
+        assert np.allclose(a, b, rtol=0, atol=0)
+    ref3 = np.array([[0.0, 0.0], [10.0, 0.0], [20.0, 10.0]])
+    a = SampleReferTraj.getShortestDistance(ref3[:, 0], ref3[:, 1], 25.0, 20.0)
+    b = R.shortest_distance(ref3[:, 0], ref3[:, 1], 25.0, 20.0, strict_xor_quirk=False)
+    assert np.allclose(a, b, rtol=0, atol=1e-15)
+    p = SampleReferTraj.Projection2D(0.0, 0.0, 0.0, 0.0, 3.0, 4.0)
+    assert p == (0.0, 0.0, 5.0, 0, 0.0)
+
+
+def test_sampler_argument_check_raises_before_launch():
+    with pytest.raises(AssertionError):
+        SampleReferTraj.sampleReferenceTrajectory(5, np.array([[0, 0], [1, 0]]), 0.0, 0.0, 1.6)
+
+
+def test_delay_compensation_matches_straight_line_and_odeint():
+    sc = _circle(4, hp=20)
+    nT = sc.ticks_delay_x + sc.ticks_per_sim + sc.ticks_delay_u
+    x_meas = np.array(sc.x0).reshape(4, 6)
+    u_path = np.zeros((4, nT))
+    x0, u0, traj = MPC_Iter.delay_compensate(sc, x_meas, u_path)
+    nominal = BT.delay_compensated_nominal(sc)
+    assert np.allclose(x0, nominal, atol=1e-6)
+    assert traj.shape == (10, 6, 4) and np.array_equal(traj[-1].T, x0)
+    assert np.all(u0 == 0)
+    with pytest.raises(AssertionError):
+        MPC_Iter.delay_compensate(sc, x_meas, np.zeros((4, nT + 1)))
+
+
+def test_obstacle_prediction_matches_restatement():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 12
+    sc.get_frog_scenario()
+    sc.complete_scenario()
+    o = R.frog_scenario(Hp=12)
+    st = np.asarray(sc.obstacles).reshape(sc.nObst, 6)[:, :2] + 0.5
+    a = MPC_Iter.predict_obstacles(sc, st)
+    b = R.obstacle_future(o, st, 12)
+    assert np.allclose(a, b, rtol=1e-15, atol=1e-13)
+    c = BT.obstacle_prediction(sc, 12, st)
+    assert np.allclose(c, b, rtol=1e-15, atol=1e-13)
+
+
+def test_batch_generation_is_deterministic_and_shard_independent():
+    sc = _circle(4, hp=20)
+    a = BT.make_batch(sc, 8, base_seed=3)
+    b = BT.make_batch(sc, 4, base_seed=3, offset=4)
+    assert np.array_equal(a.x0[4:], b.x0) and np.array_equal(a.ec_noise[4:], b.ec_noise)
+    assert a.x0.shape == (8, 4, 6) and a.ec_noise.shape == (8, 4, 2) and a.hp.dtype == np.int32
+    d = a.x0 - BT.delay_compensated_nominal(sc)[None]
+    assert np.all(d[:, :, 4] == 0)
+    assert abs(d[:, :, 0].std() - 0.05) < 0.03
+    m = BT.make_batch(sc, 6, mixed_hp=(10, 20, 30))
+    assert m.hp.tolist() == [10, 20, 30, 10, 20, 30] and m.hp_max == 30
+
+
+def test_mixed_horizon_obstacle_slots_are_packed():
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 30
+    sc.get_parallel_scenario(3)
+    sc.complete_scenario()
+    bt = BT.make_batch(sc, 3, mixed_hp=(10, 20, 30))
+    for b, H in enumerate((10, 20, 30)):
+        want = BT.obstacle_prediction(sc, H).reshape(-1)
+        slot = bt.obst[b].reshape(-1)
+        assert np.array_equal(slot[:want.size], want)
+        assert np.all(slot[want.size:] == 0)
+
+
+def test_flop_model_sizes():
+    assert FL._sizes(4, 20, 0) == (80, 81, 120, 281)
+    assert FL._sizes(8, 30, 0) == (240, 241, 840, 1321)
+    assert FL.factor(81) == 81 ** 3 // 3
+    f = FL.problem_flops(4, 20, 0, 7, 109)
+    assert 5e7 < f < 1e8
+    assert FL.batch_flops(4, [20, 20], 0, [7, 7], [109, 109]) == 2 * f
+    assert FL.compulsory_bytes(4, 20, 0) > 0
+
+
+def test_config_and_miqp_stub():
+    assert Config.Config().QCQP.constraintTolerance == pytest.approx(0.0042)
+    with pytest.raises(NotImplementedError):
+        MIQP.MIQPcontroller(None, None, None)

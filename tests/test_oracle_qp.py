@@ -1,0 +1,99 @@
+"""The oracle's QP step against an independent solver (scipy trust-constr) and its own
+KKT certificate.  The convexified QP has a unique
+minimiser, so agreement with any accurate solver pins the answer
+GUROBI returns in the reference (SCP_controller.py:135-146)."""
+import math
+
+import numpy as np
+import pytest
+import scipy.optimize
+
+from oracle import scp_reference as R
+
+
+def _qp_instance(n_veh, hp, seed, u_lin_scale=0.02):
+    sc = R.circle_scenario(n_veh, Hp=hp)
+    g = np.random.default_rng(seed)
+    x0 = np.array(sc.x0)
+    for v in range(n_veh):
+        # close the circle so the pairs interact within the horizon
+        x0[v, 0] *= 0.45
+        x0[v, 1] *= 0.45
+    x0 += g.normal(0, 0.05, x0.shape) * [1, 1, 0.1, 0.2, 0, 0.02]
+    p = R.make_problem(sc, x0, ec_noise=g.normal(0, 3e-6, (n_veh, 2)))
+    L = R.linearise(p, "structured")
+    u_lin = g.uniform(-u_lin_scale, u_lin_scale, n_veh * hp)
+    A, b = R.linearised_rows_structured(p, L, u_lin)
+    N = n_veh * hp
+    Phi0 = np.zeros((N, N))
+    Psi0 = np.zeros(N)
+    for v in range(n_veh):
+        Phi0[v * hp:(v + 1) * hp, v * hp:(v + 1) * hp] = L.Phi0[v]
+        Psi0[v * hp:(v + 1) * hp] = L.Psi0[v]
+    return sc, R.qp_matrices(Phi0, Psi0, A, b, sc.uLim), N
+
+
+@pytest.mark.parametrize("n_veh,hp,seed", [(3, 8, 0), (3, 8, 1), (4, 6, 2)])
+def test_qp_matches_scipy(n_veh, hp, seed):
+    sc, (P, q, G, h), N = _qp_instance(n_veh, hp, seed)
+    res = R.qp_solve(P, q, G, h, sc.uLim, N)
+    assert res.converged or res.polished
+    # trust-constr on the same problem, variables scaled to units of uLim for conditioning
+    s = np.ones(N + 1)
+    s[:N] = sc.uLim
+    Ps, qs, Gs = P * s[:, None] * s[None, :], q * s, G * s[None, :]
+    f = lambda x: 0.5 * x @ Ps @ x + qs @ x          # noqa: E731
+    x0 = np.zeros(N + 1)
+    x0[N] = 10.0
+    sol = scipy.optimize.minimize(f, x0, jac=lambda x: Ps @ x + qs, hess=lambda x: Ps,
+                                  constraints=[scipy.optimize.LinearConstraint(Gs, -np.inf, h)],
+                                  method="trust-constr",
+                                  options={"gtol": 1e-12, "xtol": 1e-14, "maxiter": 20000})
+    assert np.max(Gs @ sol.x - h) <= 1e-9
+    assert f(res.z / s) <= f(sol.x) + 1e-9 * abs(f(sol.x))
+    z_ref = sol.x * s
+    assert np.max(np.abs(res.z[:N] - z_ref[:N])) <= 1e-7
+    assert abs(res.z[N] - z_ref[N]) <= 1e-6 * max(1.0, abs(z_ref[N]))
+
+
+@pytest.mark.parametrize("polish", ["exact", "regularised"])
+def test_qp_certificate(polish):
+    sc, (P, q, G, h), N = _qp_instance(4, 10, 7)
+    res = R.qp_solve(P, q, G, h, sc.uLim, N, polish=polish)
+    c = res.certificate
+    assert c["primal"] <= 1e-9 * max(1.0, np.abs(h).max())
+    assert c["dual"] <= 1e-9 * max(1.0, np.abs(res.lam).max())
+    assert c["stationarity"] <= 1e-7 * max(1.0, np.abs(q).max())
+    assert c["complementarity"] <= 1e-9 * max(1.0, np.abs(res.lam).max())
+
+
+def test_polish_modes_agree():
+    sc, (P, q, G, h), N = _qp_instance(4, 12, 11)
+    a = R.qp_solve(P, q, G, h, sc.uLim, N, polish="exact")
+    b = R.qp_solve(P, q, G, h, sc.uLim, N, polish="regularised")
+    c = R.qp_solve(P, q, G, h, sc.uLim, N, polish=None)
+    assert np.max(np.abs(a.z[:N] - b.z[:N])) <= 1e-9
+    assert np.max(np.abs(a.z[:N] - c.z[:N])) <= 1e-7
+
+
+def test_slack_is_inactive_when_feasible_and_box_respected():
+    sc, (P, q, G, h), N = _qp_instance(2, 10, 5, u_lin_scale=0.0)
+    res = R.qp_solve(P, q, G, h, sc.uLim, N)
+    assert np.all(np.abs(res.z[:N]) <= sc.uLim * (1 + 1e-12))
+    assert res.z[N] >= -1e-12
+
+
+def test_faithful_and_structured_scp_agree():
+    sc = R.circle_scenario(4, Hp=20)
+    g = np.random.default_rng(5)
+    x0 = np.array(sc.x0)
+    for v in range(4):
+        x0[v, 0] += 1.72 * math.cos(x0[v, 2])
+        x0[v, 1] += 1.72 * math.sin(x0[v, 2])
+    x0 += g.normal(0, 1, x0.shape) * [0.05, 0.05, 0.005, 0.02, 0, 0.002]
+    p = R.make_problem(sc, x0, ec_noise=g.normal(0, 3e-6, (4, 2)))
+    a = R.scp_solve(p, mode="faithful")
+    b = R.scp_solve(p, mode="structured")
+    assert a.n_scp == b.n_scp
+    assert np.max(np.abs(a.u - b.u)) <= 1e-8
+    assert np.max(np.abs(a.traj - b.traj)) <= 1e-7
