@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (config c2: 1024)")
     ap.add_argument("--n-veh", type=int, default=4)
     ap.add_argument("--hp", type=int, default=20)
-    ap.add_argument("--cpu-sample", type=int, default=128)
+    ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
 

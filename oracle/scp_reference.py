@@ -792,49 +792,85 @@ def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60):
     return x, s, lam, maxit, 0
 
 
-def _polish_ok(G, h, x, lam_act, tol=1e-9):
-    if (G @ x - h).max() > tol * max(1.0, np.abs(h).max()):
-        return False
-    return not (lam_act.size and lam_act.min() < -tol * max(1.0, np.abs(lam_act).max()))
+POLISH_ROUNDS = 6           # active-set corrections of the polish (primal-dual active set)
 
 
-def qp_polish_exact(P, q, G, h, x, s, lam):
-    """Solve [P G_A'; G_A 0][x; y] = [-q; h_A] directly; keep it if it certifies."""
+def _pdas_update(G, h, act, xp, lam_act, tol=1e-9):
+    """One primal-dual active-set correction: add violated inactive rows, drop
+    active rows with negative multipliers.  Returns (certified, new active set).
+
+    The IPM may stop early (normal-matrix breakdown near the end of the central
+    path, or its iteration cap) with rows still undecided; {lam > s} is then a
+    guess and the polish corrects it in a few rounds (Hintermueller, Ito &
+    Kunisch 2002 semismooth-Newton view of active-set updates).
+    """
+    r = G @ xp - h
+    hn = max(1.0, np.abs(h).max())
+    lam_full = np.zeros(len(h)); lam_full[act] = lam_act
+    viol = r > tol * hn
+    neg = act & (lam_full < -tol * max(1.0, np.abs(lam_act).max() if lam_act.size else 1.0))
+    if not viol.any() and not neg.any():
+        return True, act
+    return False, (act & ~neg) | viol
+
+
+def qp_polish_exact(P, q, G, h, x, s, lam, rounds=POLISH_ROUNDS):
+    """Solve [P G_A'; G_A 0][x; y] = [-q; h_A] on the active set A = {lam > s},
+    correcting A until the point certifies (primal feasible, y >= 0)."""
     act = lam > s
-    Ga, ha = G[act], h[act]
-    n, na = len(q), int(act.sum())
-    K = np.zeros((n + na, n + na))
-    K[:n, :n] = P; K[:n, n:] = Ga.T; K[n:, :n] = Ga
-    rhs = np.concatenate([-q, ha])
-    try:
-        sol = np.linalg.solve(K, rhs)
-    except np.linalg.LinAlgError:
-        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
-    xp, la = sol[:n], sol[n:]
-    if not np.all(np.isfinite(sol)) or not _polish_ok(G, h, xp, la):
-        return None
-    lam_full = np.zeros_like(lam); lam_full[act] = la
-    return xp, lam_full
+    n = len(q)
+    for _ in range(rounds):
+        Ga, ha = G[act], h[act]
+        na = int(act.sum())
+        K = np.zeros((n + na, n + na))
+        K[:n, :n] = P; K[:n, n:] = Ga.T; K[n:, :n] = Ga
+        rhs = np.concatenate([-q, ha])
+        try:
+            sol = np.linalg.solve(K, rhs)
+        except np.linalg.LinAlgError:
+            sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+        if not np.all(np.isfinite(sol)):
+            return None
+        xp, la = sol[:n], sol[n:]
+        ok, nxt = _pdas_update(G, h, act, xp, la)
+        if ok:
+            lam_full = np.zeros_like(lam); lam_full[act] = la
+            return xp, lam_full
+        if np.array_equal(nxt, act):
+            return None
+        act = nxt
+    return None
 
 
 def qp_polish_regularised(P, q, G, h, x, s, lam, delta=POLISH_DELTA, rho=POLISH_RHO,
-                          nref=POLISH_REFINE):
-    """Proximal method-of-multipliers polish on the active set (what the HIP kernel does)."""
+                          nref=POLISH_REFINE, rounds=POLISH_ROUNDS):
+    """Proximal method-of-multipliers polish on the active set, with the same
+    primal-dual active-set corrections (what the HIP kernel does)."""
     act = lam > s
-    Ga, ha = G[act], h[act]
-    y = lam[act].copy()
-    try:
-        L = np.linalg.cholesky(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta)
-    except np.linalg.LinAlgError:
-        return None
+    y_all = np.where(act, lam, 0.0)
     xk = x.copy()
-    for _ in range(nref):
-        xk = scipy.linalg.cho_solve((L, True), -q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
-        y = y + (Ga @ xk - ha) / delta
-    if not _polish_ok(G, h, xk, y):
-        return None
-    lam_full = np.zeros_like(lam); lam_full[act] = y
-    return xk, lam_full
+    for _ in range(rounds):
+        Ga, ha = G[act], h[act]
+        y = y_all[act].copy()
+        try:
+            L = np.linalg.cholesky(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta)
+        except np.linalg.LinAlgError:
+            return None
+        for _ in range(nref):
+            xk = scipy.linalg.cho_solve((L, True), -q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
+            y = y + (Ga @ xk - ha) / delta
+        if not np.all(np.isfinite(xk)):
+            return None
+        ok, nxt = _pdas_update(G, h, act, xk, y)
+        if ok:
+            lam_full = np.zeros_like(lam); lam_full[act] = y
+            return xk, lam_full
+        if np.array_equal(nxt, act):
+            return None
+        y_all = np.zeros(len(h)); y_all[act] = y
+        y_all[~nxt] = 0.0            # dropped rows leave, added rows start at y = 0
+        act = nxt
+    return None
 
 
 def kkt_residuals(P, q, G, h, x, lam):

@@ -91,6 +91,7 @@ class SCPcontroller:
         status = int(res.status[0].item())
         log = {'status': status & 0xff, 'flags': status & ~0xff,
                'n_scp': int(res.n_scp[0].item()), 'n_ipm': int(res.n_ipm[0].item()),
+               'obj': float(res.obj[0].item()),
                'max_violation': float(res.max_violation[0].item()),
                'sum_violations': float(res.sum_violations[0].item())}
         self._last_traj = res.traj[0, :self.Hp].cpu().numpy()

