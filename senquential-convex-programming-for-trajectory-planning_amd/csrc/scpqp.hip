@@ -226,30 +226,48 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
                                 (static_cast<unsigned int>(lo)));
 }
 
-__device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Wave-wide reductions on DPP lane moves (VALU only; no LDS round trip as
+// with ds_bpermute): quad xor 1 / xor 2, half-row and row mirrors combine 16
+// lanes, then row_bcast:15 / row_bcast:31 carry rows 0..2 into lane 63.
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_d(double v, double old) {
+    const long long b = __double_as_longlong(v), o = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)(o & 0xffffffffll), (int)(b & 0xffffffffll),
+                                               CTRL, RMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, RMASK, 0xf,
+                                               false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ double wave_max(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o, 64));
-    return v;
+template <bool MAX>
+__device__ __forceinline__ double wave_reduce(double v) {
+    const double id = MAX ? -INFINITY : 0.0;
+    auto op = [](double a, double b) { return MAX ? fmax(a, b) : a + b; };
+    v = op(v, dpp_d<0xb1, 0xf>(v, id));    // quad_perm [1,0,3,2]
+    v = op(v, dpp_d<0x4e, 0xf>(v, id));    // quad_perm [2,3,0,1]
+    v = op(v, dpp_d<0x141, 0xf>(v, id));   // row_half_mirror
+    v = op(v, dpp_d<0x140, 0xf>(v, id));   // row_mirror
+    v = op(v, dpp_d<0x142, 0xa>(v, id));   // row_bcast:15 -> rows 1, 3
+    v = op(v, dpp_d<0x143, 0xc>(v, id));   // row_bcast:31 -> rows 2, 3
+    return readlane_d(v, 63);
 }
+__device__ __forceinline__ double wave_sum(double v) { return wave_reduce<false>(v); }
+__device__ __forceinline__ double wave_max(double v) { return wave_reduce<true>(v); }
 
 // Reduce four values across the workgroup; bit q of maxmask: max, else sum.
+// NQ: number of leading slots in use (the rest are left untouched).
+template <int NQ = 4>
 __device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldouble* red) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = (maxmask >> q & 1) ? wave_max(v[q]) : wave_sum(v[q]);
+    for (int q = 0; q < NQ; ++q) v[q] = (maxmask >> q & 1) ? wave_max(v[q]) : wave_sum(v[q]);
     __syncthreads();
     if (l == 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q) red[w * 4 + q] = v[q];
+        for (int q = 0; q < NQ; ++q) red[w * 4 + q] = v[q];
     }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
+    for (int q = 0; q < NQ; ++q) {
         double r = red[q];
 #pragma unroll
         for (int ww = 1; ww < NWAVE; ++ww)
@@ -722,7 +740,7 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
     }
     for (int r = tid; r < L.m; r += NT) wsum += t[r] * L.rowW[r];
     double red[4] = {wsum, 0.0, 0.0, 0.0};
-    block_reduce4(red, 0, L.red);   // barriers: yb visible afterwards
+    block_reduce4<1>(red, 0, L.red);   // barriers: yb visible afterwards
     for (int e = tid; e < L.N; e += NT) {
         const int v = e / L.Hb, l = e % L.Hb;
         out[e] = toeplitz_t_entry(L, L.yb, v, l) + t[L.m + e] - t[L.m + L.N + e];
@@ -786,7 +804,7 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
     double ww = 0.0;
     for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
     double red[4] = {ww, 0.0, 0.0, 0.0};
-    block_reduce4(red, 0, L.red);
+    block_reduce4<1>(red, 0, L.red);
     // phase 2: K_uu lower triangle, omega row, omega diagonal
     const int N = L.N, ld = L.ld;
     const int ty = tid / TXD, tx = tid % TXD;
@@ -959,7 +977,7 @@ __device__ bool cholesky(const LT& L) {
 
 template <int R, class HP>
 struct Solver {
-    static constexpr int SCH = R <= 2 ? 8 : 4;   // chunk (columns / rows) streamed per step group
+    static constexpr int SCH = 4;   // chunk (columns / rows) streamed per step group
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
     int lane, n, ld;
@@ -1136,7 +1154,7 @@ __device__ EvalRes evaluate_u(const DevParams& P, const LT& L, const ldouble* u,
         }
     }
     double red[4] = {obj, sm, nviol, mx};
-    block_reduce4(red, 8, L.red);
+    block_reduce4<4>(red, 8, L.red);
     EvalRes res;
     res.obj = red[0];
     res.sumv = red[1];
@@ -1248,7 +1266,7 @@ __device__ void residuals(const DevParams& P, const LT& L, double (&out)[4]) {
         quad += qk * (y0 * y0 + y1 * y1);
     }
     double red[4] = {mrp, gap, wl, quad};
-    block_reduce4(red, 1, L.red);
+    block_reduce4<4>(red, 1, L.red);
     double mrd = 0.0, quad2 = 0.0, lin = 0.0;
     for (int e = tid; e < N; e += NT) {
         const int v = e / Hb, l = e % Hb;
@@ -1264,7 +1282,7 @@ __device__ void residuals(const DevParams& P, const LT& L, double (&out)[4]) {
     const double rdw = P.slackW + red[2] - L.lam[L.mc - 1];
     if (tid == 0) L.rd[N] = rdw;
     double red2[4] = {mrd, quad2, lin, 0.0};
-    block_reduce4(red2, 1, L.red);
+    block_reduce4<3>(red2, 1, L.red);
     out[0] = red[0];
     out[1] = fmax(red2[0], fabs(rdw));
     out[2] = red[1];
@@ -1280,7 +1298,7 @@ __device__ double max_step(const LT& L) {
         if (L.dl[r] < 0.0) a = fmin(a, -L.lam[r] / L.dl[r]);
     }
     double red[4] = {-a, 0.0, 0.0, 0.0};
-    block_reduce4(red, 1, L.red);
+    block_reduce4<1>(red, 1, L.red);
     return -red[0];
 }
 
@@ -1382,7 +1400,7 @@ PHASE D4 ph_init_a(Ctx c) {
     }
     for (int e = tid; e < L.n; e += NT) L.dz[e] = 0.0;
     double red[4] = {hmax, qmax, 0.0, 0.0};
-    block_reduce4(red, 3, L.red);
+    block_reduce4<2>(red, 3, L.red);
     return D4{red[0], red[1], 0.0, 0.0};
 }
 // s = h - G z, lam = -s, CVXOPT positivity shifts
@@ -1400,7 +1418,7 @@ PHASE void ph_init_b(Ctx c) {
         ssq += sv * sv;
     }
     double red[4] = {-smin, ssq, smax, 0.0};
-    block_reduce4(red, 5, L.red);
+    block_reduce4<3>(red, 5, L.red);
     const double ts = red[0], nrm = sqrt(red[1]), tz = red[2];   // tz = -min(lam) = max(s)
     const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
     const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
@@ -1452,7 +1470,7 @@ PHASE double ph_affine(Ctx c, double mu) {
         L.la[r] = L.dl[r];
     }
     double red[4] = {mua, 0.0, 0.0, 0.0};
-    block_reduce4(red, 0, L.red);
+    block_reduce4<1>(red, 0, L.red);
     const double sr = red[0] / L.mc / mu;
     return sr * sr * sr * mu;
 }
@@ -1512,7 +1530,7 @@ PHASE int ph_polish_accept(Ctx c, double hmax) {
     for (int e = tid; e < L.n; e += NT)
         if (!isfinite(L.dz[e])) nonfin = 1.0;
     double red[4] = {viol, -ymin, ymax, nonfin};
-    block_reduce4(red, 15, L.red);
+    block_reduce4<4>(red, 15, L.red);
     const double vtol = 1e-9 * hmax, ytol = -1e-9 * fmax(1.0, red[2]);
     const bool ok = red[0] <= vtol && -red[1] >= ytol && red[3] == 0.0;
     if (ok) {
@@ -1535,7 +1553,7 @@ PHASE int ph_polish_accept(Ctx c, double hmax) {
         }
     }
     double red2[4] = {changed, 0.0, 0.0, 0.0};
-    block_reduce4(red2, 1, L.red);
+    block_reduce4<1>(red2, 1, L.red);
     return red2[0] != 0.0 ? 2 : 0;
 }
 // u-bar <- uLim * z  (unscaled controls of the QP solution)

@@ -14,21 +14,30 @@ LIB_PATH = os.path.join(_PKG, "libscpqp.so")
 ARCH = os.environ.get("SCPQP_ARCH", "gfx950")
 
 
-def build_library(force=False, verbose=False):
-    """Compile with hipcc unless the .so is newer than its sources."""
+def build_library(force=False, verbose=False, defines=(), out=None):
+    """Compile with hipcc unless the .so is newer than its sources.
+
+    ``defines``/``out`` build a diagnostic variant (e.g. ``("SCPQP_PROF",)`` ->
+    ``libscpqp_prof.so``); the shipped library is built with neither."""
+    out = out or LIB_PATH
     deps = [SRC, os.path.join(INCLUDE, "scpqp.h"), __file__]
-    if not force and os.path.exists(LIB_PATH):
-        t = os.path.getmtime(LIB_PATH)
+    if not force and os.path.exists(out):
+        t = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= t for d in deps):
-            return LIB_PATH
+            return out
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-Wno-unused-result", f"-I{INCLUDE}", SRC, "-o", LIB_PATH + ".tmp"]
+           "-Wno-unused-result", f"-I{INCLUDE}"] + [f"-D{d}" for d in defines] + \
+          [SRC, "-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(LIB_PATH + ".tmp", LIB_PATH)
-    return LIB_PATH
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build_library(force="--force" in sys.argv, verbose=True))
+    if "--prof" in sys.argv:
+        print(build_library(force="--force" in sys.argv, verbose=True, defines=("SCPQP_PROF",),
+                            out=os.path.join(_PKG, "libscpqp_prof.so")))
+    else:
+        print(build_library(force="--force" in sys.argv, verbose=True))
