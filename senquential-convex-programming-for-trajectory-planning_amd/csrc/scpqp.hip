@@ -163,7 +163,8 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.persist = p;
     f.scr = p;
     int u = 0, w = 0;
-    if (hG) { f.H = w; w += pad2(roff(n) + 16); } else { f.H = p + u; u += pad2(roff(n) + 16); }
+    // packed K plus one spare row (row n: target of the predicate-free tile stores)
+    if (hG) { f.H = w; w += pad2(roff(n + 1) + 16); } else { f.H = p + u; u += pad2(roff(n + 1) + 16); }
     f.Wt = p + u; u += pad2(4 * Hm * nb);
     if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     const int setup = NWAVE * SCR_PER_WAVE;
@@ -856,56 +857,68 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
 // ---------------------------------------------------------------------------
 #define CB 8
 
+// 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
+// a fraction of the IEEE division sequence's latency on the serial panel path).
+__device__ __forceinline__ double recip(double x) {
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+}
+
 __device__ __forceinline__ bool wave0() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;   // wave-uniform branch
 }
 
 template <class LT>
 __device__ bool cholesky(const LT& L) {
-    const int tid = threadIdx.x, n = L.n, ld = L.ld;
+    const int tid = threadIdx.x;
+    const int n = __builtin_amdgcn_readfirstlane(L.n);
     const int ty = tid / TXD, tx = tid % TXD;
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
     lint* flag = (lint*)(L.red + 120);
     ldouble* dvec = L.red + 64;   // pivots of the current panel (CB)
+    PROF_T0();
     for (int j0 = 0; j0 < n; j0 += CB) {
         const int jb = min(CB, n - j0);
         if (wave0()) {
+            // Panel in registers, rows i = j0 + lane + 64 t.  Branch-free: rows
+            // >= n load zeros, columns >= jb of the last panel are padded with an
+            // identity block (D = 1, no coupling), and updates of entries above
+            // the diagonal (lane < c2) only touch values that are never broadcast
+            // or stored.
             const int lane = tid;
             double p[RS][CB];
 #pragma unroll
             for (int t = 0; t < RS; ++t) {
                 const int i = j0 + lane + 64 * t;
+                const int ir = i < n ? i : n - 1;
 #pragma unroll
                 for (int c = 0; c < CB; c += 2) {
-                    double2v v = {0.0, 0.0};
-                    if (i < n && c < jb) v = ld2(L.H + roff(i) + j0 + c);
-                    p[t][c] = v.x;
-                    p[t][c + 1] = v.y;
+                    const double2v v = ld2(L.H + roff(ir) + j0 + c);
+                    p[t][c] = (i < n && c < jb) ? v.x : ((t == 0 && lane == c) ? 1.0 : 0.0);
+                    p[t][c + 1] =
+                        (i < n && c + 1 < jb) ? v.y : ((t == 0 && lane == c + 1) ? 1.0 : 0.0);
                 }
             }
             int bad = 0;
 #pragma unroll
             for (int c = 0; c < CB; ++c) {
-                if (c < jb) {
-                    const double D = readlane_d(p[0][c], c);
-                    bad |= !(D > 0.0) || !isfinite(D);
-                    const double inv = 1.0 / D;
+                const double D = readlane_d(p[0][c], c);
+                bad |= !(D > 0.0) || !isfinite(D);
+                const double inv = recip(D);
 #pragma unroll
-                    for (int c2 = c + 1; c2 < CB; ++c2) {
-                        if (c2 < jb) {
-                            const double lc = readlane_d(p[0][c], c2) * inv;
+                for (int c2 = c + 1; c2 < CB; ++c2) {
+                    const double lc = readlane_d(p[0][c], c2) * inv;
 #pragma unroll
-                            for (int t = 0; t < RS; ++t)
-                                if (lane + 64 * t >= c2) p[t][c2] -= p[t][c] * lc;
-                        }
-                    }
+                    for (int t = 0; t < RS; ++t) p[t][c2] -= p[t][c] * lc;
+                }
 #pragma unroll
-                    for (int t = 0; t < RS; ++t)
-                        if (lane + 64 * t > c) p[t][c] *= inv;
-                    if (lane == 0) {
-                        L.dinv[j0 + c] = inv;
-                        dvec[c] = D;
-                    }
+                for (int t = 0; t < RS; ++t) p[t][c] *= inv;
+                if (lane == 0 && c < jb) {
+                    L.dinv[j0 + c] = inv;
+                    dvec[c] = D;
                 }
             }
 #pragma unroll
@@ -920,49 +933,51 @@ __device__ bool cholesky(const LT& L) {
             if (lane == 0) flag[0] = bad;
         }
         __syncthreads();
+        PROF_ACC(12);
         if (flag[0]) return false;
+        // Rank-CB trailing update H_ik -= sum_c L_ic D_c L_kc in 2x2 register
+        // tiles.  r0 is even, so the (i0, i0 + 1) element of a diagonal tile is
+        // row i0's padding slot, and row n (i1 == n) is the spare row the plan
+        // allocates: the tile stores need no predicates.
         const int r0 = j0 + jb;
         if (r0 < n) {
             double dc[CB];
 #pragma unroll
-            for (int c = 0; c < CB; ++c) dc[c] = c < jb ? dvec[c] : 0.0;
+            for (int c = 0; c < CB; ++c) dc[c] = dvec[c];
             const int T = (n - r0 + 1) >> 1;
             for (int ti = ty; ti < T; ti += TYD) {
-                const int i0 = r0 + 2 * ti, i1 = i0 + 1;
-                const int o0 = roff(i0), o1 = roff(i1);
+                const int i0 = r0 + 2 * ti;
+                const int o0 = roff(i0), o1 = roff(i0 + 1);
                 double a0[CB], a1[CB];
 #pragma unroll
                 for (int c = 0; c < CB; c += 2) {
                     const double2v u = ld2(L.H + o0 + j0 + c);
-                    double2v w = {0.0, 0.0};
-                    if (i1 < n) w = ld2(L.H + o1 + j0 + c);
+                    const double2v w = ld2(L.H + o1 + j0 + c);
                     a0[c] = u.x * dc[c]; a0[c + 1] = u.y * dc[c + 1];
                     a1[c] = w.x * dc[c]; a1[c + 1] = w.y * dc[c + 1];
                 }
                 for (int tk = tx; tk <= ti; tk += TXD) {
-                    const int k0 = r0 + 2 * tk, k1 = k0 + 1;
-                    const int q0 = roff(k0), q1 = roff(k1);
+                    const int k0 = r0 + 2 * tk;
+                    const int q0 = roff(k0), q1 = roff(k0 + 1);
                     double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
 #pragma unroll
                     for (int c = 0; c < CB; c += 2) {
                         const double2v u = ld2(L.H + q0 + j0 + c);
-                        double2v w = {0.0, 0.0};
-                        if (k1 < n) w = ld2(L.H + q1 + j0 + c);
+                        const double2v w = ld2(L.H + q1 + j0 + c);
                         s00 += a0[c] * u.x + a0[c + 1] * u.y;
                         s01 += a0[c] * w.x + a0[c + 1] * w.y;
                         s10 += a1[c] * u.x + a1[c + 1] * u.y;
                         s11 += a1[c] * w.x + a1[c + 1] * w.y;
                     }
                     L.H[o0 + k0] -= s00;
-                    if (k1 <= i0) L.H[o0 + k1] -= s01;
-                    if (i1 < n) {
-                        L.H[o1 + k0] -= s10;
-                        if (k1 < n) L.H[o1 + k1] -= s11;
-                    }
+                    L.H[o0 + k0 + 1] -= s01;
+                    L.H[o1 + k0] -= s10;
+                    L.H[o1 + k0 + 1] -= s11;
                 }
             }
         }
         __syncthreads();
+        PROF_ACC(13);
     }
     return true;
 }
@@ -981,10 +996,14 @@ struct Solver {
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
     int lane, n, ld;
-    double r[R];
-    int ii[R], ro[R];
+    double r[R], xf[R];
+    int ii[R], ro[R], ic[R];
     double cur[R][SCH], nxt[R][SCH];
 
+    // No per-lane predicates in the step loops: rows of a lane that is already
+    // final (i <= j in the forward sweep, i >= j backward) read entries past
+    // their row end and accumulate garbage, so every final value is captured
+    // into xf at the step that produces it.  Rows >= n read a clamped row.
     __device__ __forceinline__ Solver(HP H_, const ldouble* dinv_, int n_, int ld_,
                                       const ldouble* bvec)
         : H(H_), dinv(dinv_), n(n_), ld(ld_) {
@@ -992,8 +1011,10 @@ struct Solver {
 #pragma unroll
         for (int t = 0; t < R; ++t) {
             ii[t] = lane + 64 * t;
-            ro[t] = roff(ii[t]);
+            ic[t] = ii[t] < n ? ii[t] : n - 1;
+            ro[t] = roff(ic[t]);
             r[t] = ii[t] < n ? bvec[ii[t]] : 0.0;
+            xf[t] = 0.0;
         }
     }
     __device__ __forceinline__ void load_cols(double (&dst)[R][SCH], int jc) {
@@ -1001,18 +1022,18 @@ struct Solver {
         for (int t = 0; t < R; ++t)
 #pragma unroll
             for (int q = 0; q < SCH; q += 2) {
-                double2v v = {0.0, 0.0};
-                if (ii[t] < n && jc + q < n) v = ld2(H + ro[t] + jc + q);
-                dst[t][q] = (ii[t] > jc + q) ? v.x : 0.0;
-                dst[t][q + 1] = (ii[t] > jc + q + 1) ? v.y : 0.0;
+                const double2v v = ld2(H + ro[t] + jc + q);
+                dst[t][q] = v.x;
+                dst[t][q + 1] = v.y;
             }
     }
     __device__ __forceinline__ void load_rows(double (&dst)[R][SCH], int jc) {
 #pragma unroll
-        for (int q = 0; q < SCH; ++q)
+        for (int q = 0; q < SCH; ++q) {
+            const int row = jc + q < n ? jc + q : n - 1;
 #pragma unroll
-            for (int t = 0; t < R; ++t)
-                dst[t][q] = (jc + q < n && ii[t] < jc + q) ? H[roff(jc + q) + ii[t]] : 0.0;
+            for (int t = 0; t < R; ++t) dst[t][q] = H[roff(row) + ic[t]];
+        }
     }
     __device__ __forceinline__ void shift() {
 #pragma unroll
@@ -1020,7 +1041,7 @@ struct Solver {
 #pragma unroll
             for (int q = 0; q < SCH; ++q) cur[t][q] = nxt[t][q];
     }
-    // forward over the columns owned by slot T (compile-time owner)
+    // forward over the columns owned by slot T (compile-time owner); slots < T are final
     template <int T>
     __device__ __forceinline__ void fwd() {
         if constexpr (T < R) {
@@ -1032,14 +1053,16 @@ struct Solver {
                     const int j = jc + q;
                     if (j < jend) {
                         const double xj = readlane_d(r[T], j & 63);
+                        xf[T] = (lane == (j & 63)) ? xj : xf[T];
 #pragma unroll
-                        for (int t = 0; t < R; ++t) r[t] -= cur[t][q] * xj;
+                        for (int t = T; t < R; ++t) r[t] -= cur[t][q] * xj;
                     }
                 }
                 shift();
             }
         }
     }
+    // backward over the rows owned by slot T; slots > T are final
     template <int T>
     __device__ __forceinline__ void bwd(int jlast) {
         if constexpr (T < R) {
@@ -1051,8 +1074,9 @@ struct Solver {
                     const int j = jc + q;
                     if (j < n) {
                         const double xj = readlane_d(r[T], j & 63);
+                        xf[T] = (lane == (j & 63)) ? xj : xf[T];
 #pragma unroll
-                        for (int t = 0; t < R; ++t) r[t] -= cur[t][q] * xj;
+                        for (int t = 0; t <= T; ++t) r[t] -= cur[t][q] * xj;
                     }
                 }
                 shift();
@@ -1060,20 +1084,25 @@ struct Solver {
         }
     }
     __device__ __forceinline__ void run(ldouble* x) {
+        PROF_T0();
         // forward  L y = b
         load_cols(cur, 0);
         fwd<0>(); fwd<1>(); fwd<2>(); fwd<3>();
+        PROF_ACC(14);
         // z = D^{-1} y
 #pragma unroll
-        for (int t = 0; t < R; ++t)
-            if (ii[t] < n) r[t] *= dinv[ii[t]];
+        for (int t = 0; t < R; ++t) {
+            r[t] = xf[t] * dinv[ic[t]];
+            xf[t] = 0.0;
+        }
         // backward  L' x = z
         const int jlast = ((n - 1) / SCH) * SCH;
         load_rows(cur, jlast);
         bwd<3>(jlast); bwd<2>(jlast); bwd<1>(jlast); bwd<0>(jlast);
 #pragma unroll
         for (int t = 0; t < R; ++t)
-            if (ii[t] < n) x[ii[t]] = r[t];
+            if (ii[t] < n) x[ii[t]] = xf[t];
+        PROF_ACC(15);
     }
 };
 

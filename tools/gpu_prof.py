@@ -13,7 +13,8 @@ from oracle import scp_reference as R
 from scpqp import batch as BT
 from scpqp.solver import ScpQpSolver
 names = ["ipm-loop-top", "residuals", "assemble", "cholesky", "newton(pred)", "maxstep+corr",
-         "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise"]
+         "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
+         "chol:panel", "chol:update", "solve:fwd", "solve:bwd"]   # 12-15: sub-phases of 3 / 9
 for nv, hp, B in [(4, 20, 1), (8, 30, 1)]:
     sc = R.circle_scenario(nv, Hp=hp)
     bt = BT.make_batch(sc, B, base_seed=1000)
@@ -28,5 +29,5 @@ for nv, hp, B in [(4, 20, 1), (8, 30, 1)]:
     tot = sum(buf[i] for i in range(12) if i != 9)
     nipm = out.n_ipm[0].item()
     print(f"nv={nv} hp={hp}: wall {wall*1e3:.2f} ms, nscp {out.n_scp[0].item()} nipm {nipm}")
-    for i, nme in enumerate(names):
+    for i, nme in enumerate(names):  # 12-15 are sub-phases (already inside 3 and 9)
         print(f"   {nme:15s} {buf[i]:12d} cyc  {buf[i]/max(nipm,1):10.0f}/ipm-it")

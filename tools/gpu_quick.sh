@@ -10,3 +10,6 @@ timeout -k 10 120 python tools/gpu_prof.py > $OUT/phases.txt 2>&1 || { echo "pro
 cat $OUT/phases.txt
 timeout -k 10 300 python bench.py --no-cpu > $OUT/bench.log 2>&1 || { echo "bench failed"; cat $OUT/bench.log; exit 1; }
 grep '^{' $OUT/bench.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('value', d['value'], 'kernel_ms', d['roofline']['kernel_ms'], 'frac', d['roofline']['frac'])"
+if [ -n "$PMC" ]; then
+  timeout -k 10 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE -f csv -d $OUT/pmcw -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu > $OUT/pmcw.log 2>&1 && python tools/pmc_table.py $(find $OUT/pmcw -name '*counter_collection.csv')
+fi
