@@ -167,7 +167,10 @@ def main():
     n_scp = out.n_scp.cpu().numpy()
     n_ipm = out.n_ipm.cpu().numpy()
     status = out.status.cpu().numpy()
-    flops = FL.batch_flops(args.n_veh, bt.hp, 0, n_scp, n_ipm, 10)
+    n_pol = out.n_polish.cpu().numpy()
+    n_ref = out.n_refine.cpu().numpy()
+    n_warm = out.n_warm.cpu().numpy()
+    flops = FL.batch_flops(args.n_veh, bt.hp, 0, n_scp, n_ipm, n_pol, n_ref, n_warm)
     achieved_tf = flops / (kern_ms * 1e-3) / 1e12
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
@@ -205,6 +208,8 @@ def main():
         "qp_solves_per_s": world * float(n_scp.sum()) * args.steps / elapsed,
         "mean_scp_iters": float(n_scp.mean()),
         "mean_ipm_iters_per_qp": float(n_ipm.sum() / max(n_scp.sum(), 1)),
+        "warm_certified_qp_frac": float(n_warm.sum() / max(n_scp.sum(), 1)),
+        "mean_polish_solves_per_qp": float(n_ref.sum() / max(n_scp.sum(), 1)),
         "status_converged_frac": float(np.mean((status & 0xff) == 0)),
     }
     if cpu is not None:

@@ -74,10 +74,10 @@ typedef struct scpqp_params {
     double slack_weight;     /* 1e5  (SCP_controller.py:84)                            */
     int32_t max_scp_iter;    /* 20   (SCP_controller.py:86)                            */
     int32_t max_ipm_iter;    /* IPM iteration cap per QP (e.g. 60)                     */
-    int32_t polish_refine;   /* refinement steps of the active-set polish (e.g. 10)    */
-    int32_t flags;           /* bit0: obstacle-evaluation quirk B.4 (default on)       */
+    int32_t polish_refine;   /* cap on multiplier-iteration solves per polish round (40)*/
+    int32_t flags;           /* SCPQP_FLAG_* (obstacle quirk B.4 on by default)        */
     double ipm_tol;          /* scaled KKT tolerance of the IPM (e.g. 1e-9)            */
-    double polish_delta;     /* polish penalty delta (scaled units, e.g. 1e-6)         */
+    double polish_delta;     /* polish penalty delta (scaled units, default 3e-7)      */
     double polish_rho;       /* polish proximal rho (e.g. 1e-12)                       */
     const double* lf;        /* [n_veh] scenario.Lf                                    */
     const double* lr;        /* [n_veh] scenario.Lr                                    */
@@ -91,7 +91,8 @@ typedef struct scpqp_params {
     int32_t ref_max_pts;
 } scpqp_params;
 
-#define SCPQP_FLAG_OBST_QUIRK 1
+#define SCPQP_FLAG_OBST_QUIRK 1   /* evaluate obstacles inside the v2 loop    */
+#define SCPQP_FLAG_COLD_QP 2      /* no active-set warm start between SCP iterations       */
 
 /* per-call inputs (DEVICE pointers) */
 typedef struct scpqp_batch_in {
@@ -118,6 +119,9 @@ typedef struct scpqp_batch_out {
     double* max_violation;   /* [B]                                                    */
     double* sum_violations;  /* [B]                                                    */
     int32_t* feasible;       /* [B]                                                    */
+    int32_t* n_polish;       /* [B] active-set polish rounds summed over the QPs       */
+    int32_t* n_refine;       /* [B] multiplier-iteration solves summed over the QPs    */
+    int32_t* n_warm;         /* [B] QPs certified from the previous QP's active set    */
 } scpqp_batch_out;
 
 /* outputs of scpqp_linearize (MPCclass intermediates; DEVICE pointers, any may be NULL) */

@@ -689,9 +689,10 @@ def evaluate_structured(p: Problem, lin: Linearisation, u, tol=CONSTRAINT_TOL, o
 # equality-constrained optimality system on the identified active set.
 # ---------------------------------------------------------------------------
 IPM_TOL = 1e-10
-POLISH_DELTA = 1e-6
+POLISH_DELTA = 3e-7
 POLISH_RHO = 1e-12
-POLISH_REFINE = 10
+POLISH_REFINE = 40          # cap on multiplier-iteration solves per polish round
+POLISH_TOL = 1e-10          # the iteration stops once max|x_k - x_{k-1}| <= tol max(1, |x_k|)
 
 
 @dataclass
@@ -845,7 +846,9 @@ def qp_polish_exact(P, q, G, h, x, s, lam, rounds=POLISH_ROUNDS):
 def qp_polish_regularised(P, q, G, h, x, s, lam, delta=POLISH_DELTA, rho=POLISH_RHO,
                           nref=POLISH_REFINE, rounds=POLISH_ROUNDS):
     """Proximal method-of-multipliers polish on the active set, with the same
-    primal-dual active-set corrections (what the HIP kernel does)."""
+    primal-dual active-set corrections (what the HIP kernel does).  Each round
+    iterates until x stops moving (POLISH_TOL) or ``nref`` solves; only a
+    converged point can certify."""
     act = lam > s
     y_all = np.where(act, lam, 0.0)
     xk = x.copy()
@@ -856,12 +859,19 @@ def qp_polish_regularised(P, q, G, h, x, s, lam, delta=POLISH_DELTA, rho=POLISH_
             L = np.linalg.cholesky(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta)
         except np.linalg.LinAlgError:
             return None
-        for _ in range(nref):
-            xk = scipy.linalg.cho_solve((L, True), -q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
-            y = y + (Ga @ xk - ha) / delta
+        conv = False
+        for k in range(nref):
+            xn = scipy.linalg.cho_solve((L, True), -q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
+            y = y + (Ga @ xn - ha) / delta
+            step = np.abs(xn - xk).max()
+            xk = xn
+            if k >= 1 and step <= POLISH_TOL * max(1.0, np.abs(xk).max()):
+                conv = True
+                break
         if not np.all(np.isfinite(xk)):
             return None
         ok, nxt = _pdas_update(G, h, act, xk, y)
+        ok = ok and conv
         if ok:
             lam_full = np.zeros_like(lam); lam_full[act] = y
             return xk, lam_full

@@ -79,6 +79,8 @@ typedef __attribute__((address_space(1))) double2v gdouble2;
 
 // 16-byte loads (ds_read_b128 / global_load_dwordx4); callers pass even offsets
 __device__ __forceinline__ double2v ld2(const ldouble* p) { return *(const ldouble2*)p; }
+__device__ __forceinline__ void st2(ldouble* p, double2v v) { *(ldouble2*)p = v; }
+__device__ __forceinline__ void st2(gdouble* p, double2v v) { *(gdouble2*)p = v; }
 __device__ __forceinline__ double2v ld2(const gdouble* p) { return *(const gdouble2*)p; }
 
 // ---------------------------------------------------------------------------
@@ -104,7 +106,7 @@ struct KArgs {
     const double *x0, *u0, *ec, *obst, *refIn, *uWarm, *uEval;
     const int* hp;
     double *uOut, *trajOut, *obj, *maxv, *sumv;
-    int *status, *nscp, *nipm, *feas;
+    int *status, *nscp, *nipm, *feas, *npol, *nref, *nwarm;
     double *Ad, *Bd, *Ed, *gOut, *p0Out, *psiOut, *refOut;
     double *cveh, *cobs;
     double* ws;
@@ -867,6 +869,15 @@ __device__ __forceinline__ double recip(double x) {
     return fma(r, e, r);
 }
 
+// t -> (i, k) with t = i (i + 1) / 2 + k, 0 <= k <= i (lower-triangle enumeration)
+__device__ __forceinline__ void tri_decode(int t, int& i, int& k) {
+    int q = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    if ((q + 1) * (q + 2) / 2 <= t) ++q;
+    if (q * (q + 1) / 2 > t) --q;
+    i = q;
+    k = t - q * (q + 1) / 2;
+}
+
 __device__ __forceinline__ bool wave0() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;   // wave-uniform branch
 }
@@ -944,35 +955,44 @@ __device__ bool cholesky(const LT& L) {
             double dc[CB];
 #pragma unroll
             for (int c = 0; c < CB; ++c) dc[c] = dvec[c];
+            // 2x2 tiles (ti >= tk) enumerated linearly so every thread gets
+            // ceil(ntile / NT) tiles (no triangular imbalance); two tiles per
+            // pass so their LDS latencies overlap.
             const int T = (n - r0 + 1) >> 1;
-            for (int ti = ty; ti < T; ti += TYD) {
-                const int i0 = r0 + 2 * ti;
-                const int o0 = roff(i0), o1 = roff(i0 + 1);
-                double a0[CB], a1[CB];
+            const int ntile = T * (T + 1) / 2;
+            for (int t = tid; t < ntile; t += 2 * NT) {
+                const int tb = t + NT < ntile ? t + NT : t;
+                int ia[2], ka[2];
+                tri_decode(t, ia[0], ka[0]);
+                tri_decode(tb, ia[1], ka[1]);
+                double sm[2][4];
 #pragma unroll
-                for (int c = 0; c < CB; c += 2) {
-                    const double2v u = ld2(L.H + o0 + j0 + c);
-                    const double2v w = ld2(L.H + o1 + j0 + c);
-                    a0[c] = u.x * dc[c]; a0[c + 1] = u.y * dc[c + 1];
-                    a1[c] = w.x * dc[c]; a1[c + 1] = w.y * dc[c + 1];
-                }
-                for (int tk = tx; tk <= ti; tk += TXD) {
-                    const int k0 = r0 + 2 * tk;
-                    const int q0 = roff(k0), q1 = roff(k0 + 1);
+                for (int u2 = 0; u2 < 2; ++u2) {
+                    const int o0 = roff(r0 + 2 * ia[u2]), o1 = roff(r0 + 2 * ia[u2] + 1);
+                    const int q0 = roff(r0 + 2 * ka[u2]), q1 = roff(r0 + 2 * ka[u2] + 1);
                     double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
 #pragma unroll
                     for (int c = 0; c < CB; c += 2) {
-                        const double2v u = ld2(L.H + q0 + j0 + c);
-                        const double2v w = ld2(L.H + q1 + j0 + c);
-                        s00 += a0[c] * u.x + a0[c + 1] * u.y;
-                        s01 += a0[c] * w.x + a0[c + 1] * w.y;
-                        s10 += a1[c] * u.x + a1[c + 1] * u.y;
-                        s11 += a1[c] * w.x + a1[c + 1] * w.y;
+                        const double2v x0 = ld2(L.H + o0 + j0 + c), x1 = ld2(L.H + o1 + j0 + c);
+                        const double2v y0 = ld2(L.H + q0 + j0 + c), y1 = ld2(L.H + q1 + j0 + c);
+                        const double e0 = x0.x * dc[c], e1 = x0.y * dc[c + 1];
+                        const double f0 = x1.x * dc[c], f1 = x1.y * dc[c + 1];
+                        s00 += e0 * y0.x + e1 * y0.y;
+                        s01 += e0 * y1.x + e1 * y1.y;
+                        s10 += f0 * y0.x + f1 * y0.y;
+                        s11 += f0 * y1.x + f1 * y1.y;
                     }
-                    L.H[o0 + k0] -= s00;
-                    L.H[o0 + k0 + 1] -= s01;
-                    L.H[o1 + k0] -= s10;
-                    L.H[o1 + k0 + 1] -= s11;
+                    sm[u2][0] = s00; sm[u2][1] = s01; sm[u2][2] = s10; sm[u2][3] = s11;
+                }
+#pragma unroll
+                for (int u2 = 0; u2 < 2; ++u2) {
+                    if (u2 == 1 && tb == t) break;
+                    const int i0 = r0 + 2 * ia[u2], k0 = r0 + 2 * ka[u2];
+                    const int o0 = roff(i0), o1 = roff(i0 + 1);
+                    L.H[o0 + k0] -= sm[u2][0];
+                    L.H[o0 + k0 + 1] -= sm[u2][1];
+                    L.H[o1 + k0] -= sm[u2][2];
+                    L.H[o1 + k0 + 1] -= sm[u2][3];
                 }
             }
         }
@@ -1415,22 +1435,16 @@ PHASE void ph_rhs_from_tv(Ctx c, double rho) {
     for (int e = threadIdx.x; e < L.N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
     __syncthreads();
 }
-// scale factors of the termination test + initial-point setup of dd/tv
-PHASE D4 ph_init_a(Ctx c) {
+// initial-point setup of dd/tv/dz
+PHASE void ph_init_a(Ctx c) {
     LAYDEF;
     const int tid = threadIdx.x;
-    double hmax = 1.0;
-    for (int r = tid; r < L.m; r += NT) hmax = fmax(hmax, fabs(L.rowH[r]));
-    double qmax = fmax(1.0, P.slackW);
-    for (int e = tid; e < L.N; e += NT) qmax = fmax(qmax, fabs(L.qs[e]));
     for (int r = tid; r < L.mc; r += NT) {
         L.dd[r] = 1.0;
         L.tv[r] = hval(L, r);
     }
     for (int e = tid; e < L.n; e += NT) L.dz[e] = 0.0;
-    double red[4] = {hmax, qmax, 0.0, 0.0};
-    block_reduce4<2>(red, 3, L.red);
-    return D4{red[0], red[1], 0.0, 0.0};
+    __syncthreads();
 }
 // s = h - G z, lam = -s, CVXOPT positivity shifts
 PHASE void ph_init_b(Ctx c) {
@@ -1523,8 +1537,29 @@ PHASE void ph_polish_prep(Ctx c) {
         L.la[r] = act ? L.lam[r] : 0.0;   // y
         L.sa[r] = act ? 1.0 : 0.0;        // active mask
     }
-    for (int e = threadIdx.x; e < L.n; e += NT) L.dz[e] = L.z[e];
+    for (int e = threadIdx.x; e < L.n; e += NT) L.dz[e] = L.rd[e] = L.z[e];
     __syncthreads();
+}
+// warm start from the previous QP of this problem: its active set (sa) and
+// multipliers (la) on the re-linearised rows, x_0 = its solution (z)
+PHASE void ph_polish_warm(Ctx c) {
+    LAYDEF;
+    const double idl = 1.0 / P.polDelta;
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.sa[r] != 0.0 ? idl : 0.0;
+    for (int e = threadIdx.x; e < L.n; e += NT) L.dz[e] = L.rd[e] = L.z[e];
+    __syncthreads();
+}
+// termination-test scales: max(1, |h|), max(1, slack weight, |q|)
+PHASE D4 ph_scales(Ctx c) {
+    LAYDEF;
+    const int tid = threadIdx.x;
+    double hmax = 1.0;
+    for (int r = tid; r < L.m; r += NT) hmax = fmax(hmax, fabs(L.rowH[r]));
+    double qmax = fmax(1.0, P.slackW);
+    for (int e = tid; e < L.N; e += NT) qmax = fmax(qmax, fabs(L.qs[e]));
+    double red[4] = {hmax, qmax, 0.0, 0.0};
+    block_reduce4<2>(red, 3, L.red);
+    return D4{red[0], red[1], 0.0, 0.0};
 }
 PHASE void ph_polish_tv(Ctx c) {
     LAYDEF;
@@ -1532,20 +1567,30 @@ PHASE void ph_polish_tv(Ctx c) {
     for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
     __syncthreads();
 }
-// rp = G x_k - h;  y += rp / delta on the active set
-PHASE void ph_polish_dual(Ctx c) {
+// rp = G x_k - h;  y += rp / delta on the active set.  Returns
+// {max |x_k - x_{k-1}|, max |x_k|} (x_{k-1} kept in rd, dead during the polish).
+PHASE D4 ph_polish_dual(Ctx c) {
     LAYDEF;
     const double idl = 1.0 / P.polDelta;
     g_apply(L, L.dz, L.rp, true);
     for (int r = threadIdx.x; r < L.mc; r += NT)
         if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
-    __syncthreads();
+    double dmax = 0.0, xmax = 0.0;
+    for (int e = threadIdx.x; e < L.n; e += NT) {
+        const double x = L.dz[e];
+        dmax = fmax(dmax, fabs(x - L.rd[e]));
+        xmax = fmax(xmax, fabs(x));
+        L.rd[e] = x;
+    }
+    double red[4] = {dmax, xmax, 0.0, 0.0};
+    block_reduce4<2>(red, 3, L.red);
+    return D4{red[0], red[1], 0.0, 0.0};
 }
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
 // Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
 // violated inactive rows, drop the active rows with negative multipliers, and
 // rebuild the polish weights.  Returns 1 accepted, 2 corrected (retry), 0 stuck.
-PHASE int ph_polish_accept(Ctx c, double hmax) {
+PHASE int ph_polish_accept(Ctx c, double hmax, int converged) {
     LAYDEF;
     const int tid = threadIdx.x;
     double viol = -1e300, ymin = 1e300, ymax = 0.0, nonfin = 0.0;
@@ -1561,7 +1606,9 @@ PHASE int ph_polish_accept(Ctx c, double hmax) {
     double red[4] = {viol, -ymin, ymax, nonfin};
     block_reduce4<4>(red, 15, L.red);
     const double vtol = 1e-9 * hmax, ytol = -1e-9 * fmax(1.0, red[2]);
-    const bool ok = red[0] <= vtol && -red[1] >= ytol && red[3] == 0.0;
+    // a point is certified only if the multiplier iteration has also converged
+    // (stationarity), else only the active set is corrected
+    const bool ok = converged && red[0] <= vtol && -red[1] >= ytol && red[3] == 0.0;
     if (ok) {
         for (int e = tid; e < L.n; e += NT) L.z[e] = L.dz[e];
         __syncthreads();
@@ -1592,20 +1639,76 @@ PHASE void ph_take_u(Ctx c) {
     __syncthreads();
 }
 
-// Active-set corrections of the polish (oracle POLISH_ROUNDS).
+// Active-set corrections of the polish (oracle POLISH_ROUNDS), the rounds a
+// warm start may take before the IPM runs, and the multiplier iteration's
+// convergence test (oracle POLISH_TOL).
 constexpr int kPolishRounds = 6;
+constexpr int kWarmRounds = 3;
+constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: P.nRefine)
+constexpr double kPolishTol = 1e-10;
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
 // variables, x = z = [u~ (N), omega]).  Returns IPM iterations; sets *qflags.
 // ---------------------------------------------------------------------------
+struct QpStats {
+    int ipm, rounds, refine, warm_ok;
+};
+
+// Polish rounds: proximal method of multipliers on the active set in sa/la/dd,
+// refined until x stops moving (|dx| <= kPolishTol max(1, |x|), at most
+// P.nRefine solves per round), certified, else the active set is corrected
+// (primal-dual active set) and the round repeats.  Returns true if certified.
 template <bool HG, bool VG, int RM>
-__device__ __noinline__ int qp_solve(Ctx c, int* qflags) {
+__device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds, int cap,
+                                              QpStats& st) {
+    const DevParams& P = *c.P;
+    bool ok = false;
+    PROF_T0();
+    for (int round = 0; round < max_rounds && !ok; ++round) {
+        ++st.rounds;
+        PH(ph_assemble)(c, P.polRho);
+        const bool fact = PH(ph_cholesky)(c) != 0;
+        PROF_ACC(7);
+        if (!fact) break;
+        int conv = 0;
+        for (int ref = 0; ref < cap; ++ref) {
+            PH(ph_polish_tv)(c);
+            PH(ph_rhs_from_tv)(c, P.polRho);
+            PH(ph_solve)(c, 1);
+            const D4 d = PH(ph_polish_dual)(c);
+            ++st.refine;
+            if (ref >= 1 && d.a <= kPolishTol * fmax(1.0, d.b)) {
+                conv = 1;
+                break;
+            }
+        }
+        const int acc = PH(ph_polish_accept)(c, hmax, conv);
+        PROF_ACC(8);
+        ok = acc == 1;
+        if (acc == 0) break;
+    }
+    return ok;
+}
+
+// One convexified QP.  warm: try the previous QP's active set first (a few
+// polish rounds, no interior point iterations); on failure, or cold, run the
+// Mehrotra IPM from the CVXOPT initial point and polish its active set.
+template <bool HG, bool VG, int RM>
+__device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st) {
     const DevParams& P = *c.P;
     const int mc = (P.nV * (P.nV - 1) / 2 + P.nV * P.nO) * c.Hb + 2 * P.nV * c.Hb + 1;
-    // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
-    const D4 sc = PH(ph_init_a)(c);
+    const D4 sc = PH(ph_scales)(c);
     const double hmax = sc.a, qmax = sc.b;
+    if (warm) {
+        PH(ph_polish_warm)(c);
+        if (polish_rounds<HG, VG, RM>(c, hmax, kWarmRounds, kWarmRefine, st)) {
+            ++st.warm_ok;
+            return true;
+        }
+    }
+    // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
+    PH(ph_init_a)(c);
     PH(ph_assemble)(c, 0.0);
     PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
     PH(ph_rhs_from_tv)(c, 0.0);
@@ -1644,31 +1747,13 @@ __device__ __noinline__ int qp_solve(Ctx c, int* qflags) {
         PH(ph_update)(c);
         PROF_ACC(6);
     }
+    st.ipm += it;
     if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
-    // ---- active-set polish: proximal method of multipliers on {lam > s}
+    // ---- active-set polish on {lam > s}
     PH(ph_polish_prep)(c);
-#ifdef SCPQP_PROF
-    _pt = __builtin_amdgcn_s_memtime();
-#endif
-    bool ok = false;
-    for (int round = 0; round < kPolishRounds && !ok; ++round) {
-        PH(ph_assemble)(c, P.polRho);
-        const bool fact = PH(ph_cholesky)(c) != 0;
-        PROF_ACC(7);
-        if (!fact) break;
-        for (int ref = 0; ref < P.nRefine; ++ref) {
-            PH(ph_polish_tv)(c);
-            PH(ph_rhs_from_tv)(c, P.polRho);
-            PH(ph_solve)(c, 1);
-            PH(ph_polish_dual)(c);
-        }
-        const int acc = PH(ph_polish_accept)(c, hmax);
-        PROF_ACC(8);
-        ok = acc == 1;
-        if (acc == 0) break;
-    }
+    const bool ok = polish_rounds<HG, VG, RM>(c, hmax, kPolishRounds, P.nRefine, st);
     if (!ok) *qflags |= SCPQP_FL_POLISH_REJECTED;
-    return it;
+    return ok;
 }
 
 // ---------------------------------------------------------------------------
@@ -1702,6 +1787,9 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
                 if (a.status) a.status[b] = SCPQP_ST_INVALID;
                 if (a.nscp) a.nscp[b] = 0;
                 if (a.nipm) a.nipm[b] = 0;
+                if (a.npol) a.npol[b] = 0;
+                if (a.nref) a.nref[b] = 0;
+                if (a.nwarm) a.nwarm[b] = 0;
             }
             __syncthreads();
             continue;
@@ -1767,14 +1855,17 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
         EvalRes ev = PH(ph_evaluate)(c, nullptr, nullptr);
         double obj0 = ev.obj, mv0 = ev.maxv;
         const int maxScp = a.maxScp > 0 ? a.maxScp : P.maxScp;
-        int qflags = 0, nipm = 0, it = 0, status = SCPQP_ST_MAX_SCP;
+        int qflags = 0, it = 0, status = SCPQP_ST_MAX_SCP;
+        QpStats qs{0, 0, 0, 0};
+        const bool warm_on = (P.flags & SCPQP_FLAG_COLD_QP) == 0;
+        bool prev_ok = false;   // previous QP certified: its active set seeds the next one
         for (it = 0; it < maxScp; ++it) {
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
             PH(ph_linearise)(c);
             PROF_ACC(11);
-            nipm += qp_solve<HG, VG, RM>(c, &qflags);
+            prev_ok = qp_solve<HG, VG, RM>(c, &qflags, warm_on && prev_ok, qs);
             PH(ph_take_u)(c);
             ev = PH(ph_evaluate)(c, nullptr, nullptr);
             const double delta = (obj0 + P.slackW * mv0) - (ev.obj + P.slackW * ev.maxv);
@@ -1806,7 +1897,10 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
         if (tid == 0) {
             if (a.status) a.status[b] = status | qflags | (sflag_any ? SCPQP_FL_SAMPLER : 0);
             if (a.nscp) a.nscp[b] = nscp;
-            if (a.nipm) a.nipm[b] = nipm;
+            if (a.nipm) a.nipm[b] = qs.ipm;
+            if (a.npol) a.npol[b] = qs.rounds;
+            if (a.nref) a.nref[b] = qs.refine;
+            if (a.nwarm) a.nwarm[b] = qs.warm_ok;
             if (a.obj) a.obj[b] = ev.obj;
             if (a.maxv) a.maxv[b] = ev.maxv;
             if (a.sumv) a.sumv[b] = ev.sumv;
@@ -1950,7 +2044,7 @@ extern "C" {
 
 const char* scpqp_last_error(void) { return g_err; }
 
-const char* scpqp_version(void) { return "scpqp-mi355x 0.2 (gfx950, fp64)"; }
+const char* scpqp_version(void) { return "scpqp-mi355x 0.3 (gfx950, fp64)"; }
 
 int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpqp_handle** out) {
     if (!dims || !p || !out) return fail(SCPQP_E_ARG, "null argument%s");
@@ -1977,7 +2071,7 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
     P.maxPts = p->ref_max_pts > 0 ? p->ref_max_pts : 2;
     P.maxScp = p->max_scp_iter > 0 ? p->max_scp_iter : 20;
     P.maxIpm = p->max_ipm_iter > 0 ? p->max_ipm_iter : 60;
-    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 10;
+    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 40;
     P.flags = p->flags;
     P.dt = p->dt;
     P.uLim = p->u_lim;
@@ -1985,7 +2079,7 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
     P.deltaTol = p->delta_tol;
     P.slackW = p->slack_weight;
     P.ipmTol = p->ipm_tol > 0 ? p->ipm_tol : 1e-9;
-    P.polDelta = p->polish_delta > 0 ? p->polish_delta : 1e-6;
+    P.polDelta = p->polish_delta > 0 ? p->polish_delta : 3e-7;
     P.polRho = p->polish_rho >= 0 ? p->polish_rho : 1e-12;
     for (int v = 0; v < V; ++v) {
         P.Lf[v] = p->lf[v];
@@ -2053,6 +2147,9 @@ int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpq
     a.maxv = out->max_violation;
     a.sumv = out->sum_violations;
     a.feas = out->feasible;
+    a.npol = out->n_polish;
+    a.nref = out->n_refine;
+    a.nwarm = out->n_warm;
     return launch(h, a, static_cast<hipStream_t>(stream));
 }
 

@@ -25,6 +25,7 @@ FL_POLISH_REJECTED = 0x100
 FL_IPM_MAXIT = 0x200
 FL_SAMPLER = 0x400
 FLAG_OBST_QUIRK = 1
+FLAG_COLD_QP = 2
 
 _dp = C.POINTER(C.c_double)
 _ip = C.POINTER(C.c_int32)
@@ -56,7 +57,8 @@ class BatchOut(C.Structure):
     _fields_ = [("u", C.c_void_p), ("traj", C.c_void_p), ("status", C.c_void_p),
                 ("n_scp", C.c_void_p), ("n_ipm", C.c_void_p), ("obj", C.c_void_p),
                 ("max_violation", C.c_void_p), ("sum_violations", C.c_void_p),
-                ("feasible", C.c_void_p)]
+                ("feasible", C.c_void_p), ("n_polish", C.c_void_p), ("n_refine", C.c_void_p),
+                ("n_warm", C.c_void_p)]
 
 
 class LinOut(C.Structure):

@@ -69,13 +69,22 @@ def ipm_iteration(V, H, O):
     return residuals + mc + assemble(V, H, O) + factor(n) + 2 * newton + 20 * mc
 
 
-def qp_overhead(V, H, O, n_refine):
-    """Initial point + active-set polish (once per QP)."""
+def qp_init(V, H, O):
+    """CVXOPT initial point of a cold QP: assemble + factor + one solve + G x."""
     N, n, m, mc = _sizes(V, H, O)
-    init = assemble(V, H, O) + factor(n) + gt_apply(V, H, O) + solve(n) + g_apply(V, H, O) + 8 * mc
-    polish = assemble(V, H, O) + factor(n) + n_refine * (gt_apply(V, H, O) + solve(n)
-                                                         + g_apply(V, H, O) + 6 * mc)
-    return init + polish
+    return assemble(V, H, O) + factor(n) + gt_apply(V, H, O) + solve(n) + g_apply(V, H, O) + 8 * mc
+
+
+def polish_round(V, H, O):
+    """One active-set polish round: assemble + factor + certification / correction."""
+    N, n, m, mc = _sizes(V, H, O)
+    return assemble(V, H, O) + factor(n) + 6 * mc
+
+
+def polish_refine(V, H, O):
+    """One multiplier-iteration step: G' t, solve, G x - h, dual update, step norm."""
+    N, n, m, mc = _sizes(V, H, O)
+    return gt_apply(V, H, O) + solve(n) + g_apply(V, H, O) + 6 * mc + 2 * n
 
 
 def scp_iteration_extra(V, H, O):
@@ -92,17 +101,21 @@ def setup(V, H):
     return V * (expm + 2 * H * 72 + 2 * H * (H + 1) + 200)
 
 
-def problem_flops(V, H, O, n_scp, n_ipm, n_refine=10):
-    """FP64 FLOPs of one SCP solve given its QP count n_scp and summed IPM iterations n_ipm."""
-    return (setup(V, H) + toeplitz_apply(V, H) + n_scp * (scp_iteration_extra(V, H, O)
-            + qp_overhead(V, H, O, n_refine)) + n_ipm * ipm_iteration(V, H, O))
+def problem_flops(V, H, O, n_scp, n_ipm, n_polish, n_refine, n_warm):
+    """FP64 FLOPs of one SCP solve from the counters the kernel returns: QPs (n_scp),
+    IPM iterations, polish rounds, multiplier-iteration solves and warm-certified QPs
+    (which skip the IPM initial point)."""
+    cold = n_scp - n_warm
+    return (setup(V, H) + toeplitz_apply(V, H) + n_scp * scp_iteration_extra(V, H, O)
+            + cold * qp_init(V, H, O) + n_ipm * ipm_iteration(V, H, O)
+            + n_polish * polish_round(V, H, O) + n_refine * polish_refine(V, H, O))
 
 
-def batch_flops(V, hps, O, n_scp, n_ipm, n_refine=10):
-    """Sum over a batch (arrays of per-problem horizon / counts)."""
+def batch_flops(V, hps, O, n_scp, n_ipm, n_polish, n_refine, n_warm):
+    """Sum over a batch (arrays of per-problem horizon / counters)."""
     tot = 0
-    for H, s, i in zip(hps, n_scp, n_ipm):
-        tot += problem_flops(V, int(H), O, int(s), int(i), n_refine)
+    for H, s, i, p, r, w in zip(hps, n_scp, n_ipm, n_polish, n_refine, n_warm):
+        tot += problem_flops(V, int(H), O, int(s), int(i), int(p), int(r), int(w))
     return tot
 
 

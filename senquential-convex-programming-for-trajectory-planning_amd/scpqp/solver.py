@@ -48,14 +48,17 @@ class SolveResult:
     max_violation: torch.Tensor
     sum_violations: torch.Tensor
     feasible: torch.Tensor
+    n_polish: torch.Tensor   # active-set polish rounds (all QPs of the problem)
+    n_refine: torch.Tensor   # multiplier-iteration solves (all QPs)
+    n_warm: torch.Tensor     # QPs certified from the previous QP's active set
 
 
 class ScpQpSolver:
     """Scenario-bound batched SCP-QP solver on one GPU."""
 
     def __init__(self, scenario, max_batch, device=None, hp_max=None, u_lim=None,
-                 max_scp_iter=MAX_SCP_ITER, max_ipm_iter=60, ipm_tol=1e-9, polish_delta=1e-6,
-                 polish_rho=1e-12, polish_refine=10, obstacle_quirk=True):
+                 max_scp_iter=MAX_SCP_ITER, max_ipm_iter=60, ipm_tol=1e-9, polish_delta=3e-7,
+                 polish_rho=1e-12, polish_refine=40, obstacle_quirk=True, warm_start=True):
         if not torch.cuda.is_available():
             raise RuntimeError("scpqp: no GPU visible; the HIP path has no CPU fallback")
         self.lib = LB.load()
@@ -94,7 +97,8 @@ class ScpQpSolver:
                       constraint_tol=CONSTRAINT_TOL, delta_tol=DELTA_TOL, slack_weight=SLACK_WEIGHT,
                       max_scp_iter=max_scp_iter, max_ipm_iter=max_ipm_iter,
                       polish_refine=polish_refine,
-                      flags=LB.FLAG_OBST_QUIRK if obstacle_quirk else 0, ipm_tol=ipm_tol,
+                      flags=(LB.FLAG_OBST_QUIRK if obstacle_quirk else 0) |
+                      (0 if warm_start else LB.FLAG_COLD_QP), ipm_tol=ipm_tol,
                       polish_delta=polish_delta, polish_rho=polish_rho,
                       lf=_dptr(lf), lr=_dptr(lr), q=_dptr(q), q_final=_dptr(qf), r=_dptr(r),
                       dsafe_veh=_dptr(dv), dsafe_obs=_dptr(do) if nO else None,
@@ -170,7 +174,9 @@ class ScpQpSolver:
         bo = LB.BatchOut(u=_vptr(out.u), traj=_vptr(out.traj), status=_vptr(out.status),
                          n_scp=_vptr(out.n_scp), n_ipm=_vptr(out.n_ipm), obj=_vptr(out.obj),
                          max_violation=_vptr(out.max_violation),
-                         sum_violations=_vptr(out.sum_violations), feasible=_vptr(out.feasible))
+                         sum_violations=_vptr(out.sum_violations), feasible=_vptr(out.feasible),
+                         n_polish=_vptr(out.n_polish), n_refine=_vptr(out.n_refine),
+                         n_warm=_vptr(out.n_warm))
         LB.check(self.lib.scpqp_solve(self.h, B, C.byref(bi), C.byref(bo), self._stream()),
                  self.lib)
         self._last_inputs = bufs   # keep device inputs alive until the stream consumes them
@@ -184,7 +190,8 @@ class ScpQpSolver:
                            status=torch.zeros(B, **i), n_scp=torch.zeros(B, **i),
                            n_ipm=torch.zeros(B, **i), obj=torch.zeros(B, **f),
                            max_violation=torch.zeros(B, **f), sum_violations=torch.zeros(B, **f),
-                           feasible=torch.zeros(B, **i))
+                           feasible=torch.zeros(B, **i), n_polish=torch.zeros(B, **i),
+                           n_refine=torch.zeros(B, **i), n_warm=torch.zeros(B, **i))
 
     def linearize(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None):
         B, bi, bufs = self._inputs(x0, u0, ec_noise, hp, obst, ref_points, need_obst=False)

@@ -168,9 +168,12 @@ def test_flop_model_sizes():
     assert FL._sizes(4, 20, 0) == (80, 81, 120, 281)
     assert FL._sizes(8, 30, 0) == (240, 241, 840, 1321)
     assert FL.factor(81) == 81 ** 3 // 3
-    f = FL.problem_flops(4, 20, 0, 7, 109)
+    # 7 QPs, 109 IPM iterations, 8 polish rounds with 40 solves, 0 warm-certified QPs
+    f = FL.problem_flops(4, 20, 0, 7, 109, 8, 40, 0)
     assert 5e7 < f < 1e8
-    assert FL.batch_flops(4, [20, 20], 0, [7, 7], [109, 109]) == 2 * f
+    assert FL.batch_flops(4, [20, 20], 0, [7, 7], [109, 109], [8, 8], [40, 40], [0, 0]) == 2 * f
+    # a warm-certified QP skips the IPM initial point
+    assert FL.problem_flops(4, 20, 0, 7, 109, 8, 40, 3) < f
     assert FL.compulsory_bytes(4, 20, 0) > 0
 
 
