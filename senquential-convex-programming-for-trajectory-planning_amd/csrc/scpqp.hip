@@ -113,6 +113,11 @@ struct KArgs {
     long long wsStride;
     int* counter;
 };
+// The kernel argument block, addressed in the constant (kernarg) address space:
+// out-of-line functions take it by pointer without the copy to private memory
+// that taking the address of a by-value kernel parameter would force.
+typedef __attribute__((address_space(4))) const KArgs cKArgs;
+
 
 // ---------------------------------------------------------------------------
 // Memory plan: integer offsets (doubles).  Persistent LDS arrays first, then a
@@ -539,7 +544,7 @@ __device__ void expm8(ldouble* scr, bool act, ldouble* red) {
 // (MPCclass, MPC_Iter.py:59-149), scaled cost gradient, row table.
 // ---------------------------------------------------------------------------
 template <class LT>
-__device__ int setup_problem(const KArgs& a, const DevParams& P, const LT& L, int b) {
+__device__ int setup_problem(const cKArgs& a, const DevParams& P, const LT& L, int b) {
     const int tid = threadIdx.x, V = L.V, O = L.O, Hb = L.Hb, Hm = P.hpMax;
     for (int i = tid; i < 6 * V; i += NT) L.x0[i] = a.x0[(size_t)b * V * 6 + i];
     for (int i = tid; i < V; i += NT) L.u0[i] = a.u0 ? a.u0[(size_t)b * V + i] : 0.0;
@@ -652,7 +657,8 @@ __device__ int setup_problem(const KArgs& a, const DevParams& P, const LT& L, in
 // Out-of-line setup: the trigonometry and expm constants stay out of the
 // register allocation of the solve loop.
 template <bool HG, bool VG, int RM>
-__device__ __noinline__ int setup_problem_ni(const KArgs& a, gdouble* ws, int b, int Hb) {
+__device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int b, int Hb) {
+    const cKArgs& a = *ap;
     const DevParams& P = *a.P;
     const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
     const Lay<HG, VG, RM> L = make_lay<HG, VG, RM>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
@@ -1797,7 +1803,7 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
         const Ctx c{a.P, ws, Hb};
         const int V = P.nV, N = V * Hb, O = P.nO;
         PROF_T0();
-        const int sflag = setup_problem_ni<HG, VG, RM>(a, ws, b, Hb);
+        const int sflag = setup_problem_ni<HG, VG, RM>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
         PROF_ACC(10);
         const int sflag_any = __syncthreads_or(sflag);
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
