@@ -852,13 +852,16 @@ def qp_polish_regularised(P, q, G, h, x, s, lam, delta=POLISH_DELTA, rho=POLISH_
     act = lam > s
     y_all = np.where(act, lam, 0.0)
     xk = x.copy()
+    L = None
+    extended = False
     for _ in range(rounds):
         Ga, ha = G[act], h[act]
         y = y_all[act].copy()
-        try:
-            L = np.linalg.cholesky(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta)
-        except np.linalg.LinAlgError:
-            return None
+        if L is None:
+            try:
+                L = np.linalg.cholesky(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta)
+            except np.linalg.LinAlgError:
+                return None
         conv = False
         for k in range(nref):
             xn = scipy.linalg.cho_solve((L, True), -q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
@@ -871,15 +874,18 @@ def qp_polish_regularised(P, q, G, h, x, s, lam, delta=POLISH_DELTA, rho=POLISH_
         if not np.all(np.isfinite(xk)):
             return None
         ok, nxt = _pdas_update(G, h, act, xk, y)
-        ok = ok and conv
-        if ok:
+        if ok and conv:
             lam_full = np.zeros_like(lam); lam_full[act] = y
             return xk, lam_full
-        if np.array_equal(nxt, act):
-            return None
         y_all = np.zeros(len(h)); y_all[act] = y
+        if np.array_equal(nxt, act):
+            if conv or extended:
+                return None          # converged on this active set but not certified: stuck
+            extended = True          # same active set, still moving: one more batch (same factor)
+            continue
         y_all[~nxt] = 0.0            # dropped rows leave, added rows start at y = 0
         act = nxt
+        L = None
     return None
 
 

@@ -1669,14 +1669,16 @@ template <bool HG, bool VG, int RM>
 __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds, int cap,
                                               QpStats& st) {
     const DevParams& P = *c.P;
-    bool ok = false;
+    bool ok = false, refactor = true, extended = false;
     PROF_T0();
     for (int round = 0; round < max_rounds && !ok; ++round) {
         ++st.rounds;
-        PH(ph_assemble)(c, P.polRho);
-        const bool fact = PH(ph_cholesky)(c) != 0;
-        PROF_ACC(7);
-        if (!fact) break;
+        if (refactor) {
+            PH(ph_assemble)(c, P.polRho);
+            const bool fact = PH(ph_cholesky)(c) != 0;
+            PROF_ACC(7);
+            if (!fact) break;
+        }
         int conv = 0;
         for (int ref = 0; ref < cap; ++ref) {
             PH(ph_polish_tv)(c);
@@ -1692,7 +1694,12 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds
         const int acc = PH(ph_polish_accept)(c, hmax, conv);
         PROF_ACC(8);
         ok = acc == 1;
-        if (acc == 0) break;
+        // acc 2: active set corrected -> refactor;  acc 0 with the multiplier
+        // iteration still moving: same active set, keep iterating on the same
+        // factor;  acc 0 after convergence: stuck, give up
+        if (acc == 0 && (conv || extended)) break;
+        extended |= acc == 0;   // one extra batch of iterations per QP
+        refactor = acc == 2;
     }
     return ok;
 }
