@@ -284,6 +284,15 @@ __device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldoub
     }
 }
 
+// t -> (i, k) with t = i (i + 1) / 2 + k, 0 <= k <= i (lower-triangle enumeration)
+__device__ __forceinline__ void tri_decode(int t, int& i, int& k) {
+    int q = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    if ((q + 1) * (q + 2) / 2 <= t) ++q;
+    if (q * (q + 1) / 2 > t) --q;
+    i = q;
+    k = t - q * (q + 1) / 2;
+}
+
 __device__ __forceinline__ int pair_index(int i, int j, int V) {
     return i * (2 * V - i - 1) / 2 + (j - i - 1);
 }
@@ -814,36 +823,59 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
     for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
     double red[4] = {ww, 0.0, 0.0, 0.0};
     block_reduce4<1>(red, 0, L.red);
-    // phase 2: K_uu lower triangle, omega row, omega diagonal
-    const int N = L.N, ld = L.ld;
-    const int ty = tid / TXD, tx = tid % TXD;
-    for (int row = ty; row < N; row += TYD) {
-        const int a_ = row / Hb, l = row % Hb;
-        const ldouble* ga = L.g + a_ * Hb * 2;
-        for (int col = tx; col <= row; col += TXD) {
-            const int b_ = col / Hb, lp = col % Hb;
-            const ldouble* gb = L.g + b_ * Hb * 2;
-            const int k0 = l > lp ? l : lp;
-            const ldouble* W = L.Wt + 4 * (k0 * nb + a_ * (a_ + 1) / 2 + b_);
-            double acc0 = 0.0, acc1 = 0.0;
-            int k = k0;
-            for (; k + 1 < Hb; k += 2, W += 8 * nb) {
-                const double2v ga0 = ld2(ga + (k - l) * 2), ga1 = ld2(ga + (k + 1 - l) * 2);
-                const double2v gb0 = ld2(gb + (k - lp) * 2), gb1 = ld2(gb + (k + 1 - lp) * 2);
-                const double2v w0 = ld2(W), w1 = ld2(W + 2);
-                const double2v v0 = ld2(W + 4 * nb), v1 = ld2(W + 4 * nb + 2);
-                acc0 += ga0.x * (w0.x * gb0.x + w0.y * gb0.y) + ga0.y * (w1.x * gb0.x + w1.y * gb0.y);
-                acc1 += ga1.x * (v0.x * gb1.x + v0.y * gb1.y) + ga1.y * (v1.x * gb1.x + v1.y * gb1.y);
-            }
-            if (k < Hb) {
-                const double2v ga0 = ld2(ga + (k - l) * 2), gb0 = ld2(gb + (k - lp) * 2);
-                const double2v w0 = ld2(W), w1 = ld2(W + 2);
-                acc0 += ga0.x * (w0.x * gb0.x + w0.y * gb0.y) + ga0.y * (w1.x * gb0.x + w1.y * gb0.y);
-            }
-            double acc = acc0 + acc1;
-            if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
-            L.H[roff(row) + col] = acc;
+    // phase 2: K_uu lower triangle in 2x2 tiles (rows l0, l0+1 of vehicle a x
+    // columns m0, m0+1 of vehicle b, a >= b): per k one W~ block and four g
+    // blocks serve four entries.  g indices below 0 read as zero, which gives
+    // each entry its own lower summation bound max(l, l').
+    const int N = L.N;
+    const int TH = (Hb + 1) >> 1, TD = TH * (TH + 1) / 2, TO = TH * TH;
+    const int ntile = V * TD + (V * (V - 1) / 2) * TO;
+    for (int t = tid; t < ntile; t += NT) {
+        int a_, b_, lt, mt;
+        if (t < V * TD) {
+            a_ = b_ = t / TD;
+            tri_decode(t - a_ * TD, lt, mt);
+        } else {
+            const int t2 = t - V * TD, pr = t2 / TO, rem = t2 - pr * TO;
+            int i_, k_;
+            tri_decode(pr, i_, k_);
+            a_ = i_ + 1;
+            b_ = k_;
+            lt = rem / TH;
+            mt = rem - lt * TH;
         }
+        const int l0 = 2 * lt, m0 = 2 * mt;
+        const ldouble* ga = L.g + a_ * Hb * 2;
+        const ldouble* gb = L.g + b_ * Hb * 2;
+        const ldouble* W = L.Wt + 4 * (a_ * (a_ + 1) / 2 + b_);
+        double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
+        for (int k = l0 > m0 ? l0 : m0; k < Hb; ++k) {
+            const double2v a0 = ld2(ga + (k - l0) * 2);
+            const double2v b0 = ld2(gb + (k - m0) * 2);
+            double2v a1 = ld2(ga + (k - l0 - 1) * 2), b1 = ld2(gb + (k - m0 - 1) * 2);
+            if (k == l0) a1 = double2v{0.0, 0.0};
+            if (k == m0) b1 = double2v{0.0, 0.0};
+            const double2v w0 = ld2(W + 4 * k * nb), w1 = ld2(W + 4 * k * nb + 2);
+            // W g_b for both columns
+            const double p0x = w0.x * b0.x + w0.y * b0.y, p0y = w1.x * b0.x + w1.y * b0.y;
+            const double p1x = w0.x * b1.x + w0.y * b1.y, p1y = w1.x * b1.x + w1.y * b1.y;
+            c00 += a0.x * p0x + a0.y * p0y;
+            c01 += a0.x * p1x + a0.y * p1y;
+            c10 += a1.x * p0x + a1.y * p0y;
+            c11 += a1.x * p1x + a1.y * p1y;
+        }
+        const double cc[2][2] = {{c00, c01}, {c10, c11}};
+#pragma unroll
+        for (int di = 0; di < 2; ++di)
+#pragma unroll
+            for (int dj = 0; dj < 2; ++dj) {
+                const int l = l0 + di, lp = m0 + dj;
+                if (l >= Hb || lp >= Hb || (a_ == b_ && lp > l)) continue;
+                const int row = a_ * Hb + l, col = b_ * Hb + lp;
+                double acc = cc[di][dj];
+                if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
+                L.H[roff(row) + col] = acc;
+            }
     }
     for (int e = tid; e < N; e += NT) {
         const int v = e / Hb, l = e % Hb;
@@ -873,15 +905,6 @@ __device__ __forceinline__ double recip(double x) {
     r = fma(r, e, r);
     e = fma(-x, r, 1.0);
     return fma(r, e, r);
-}
-
-// t -> (i, k) with t = i (i + 1) / 2 + k, 0 <= k <= i (lower-triangle enumeration)
-__device__ __forceinline__ void tri_decode(int t, int& i, int& k) {
-    int q = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
-    if ((q + 1) * (q + 2) / 2 <= t) ++q;
-    if (q * (q + 1) / 2 > t) --q;
-    i = q;
-    k = t - q * (q + 1) / 2;
 }
 
 __device__ __forceinline__ bool wave0() {
