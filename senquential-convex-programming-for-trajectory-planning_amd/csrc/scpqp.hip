@@ -37,6 +37,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <new>
@@ -57,12 +58,12 @@ namespace {
 
 // Diagnostic phase stamps (built only with -DSCPQP_PROF; never in the shipped kernel).
 #ifdef SCPQP_PROF
-__device__ unsigned long long g_prof[16];
+__device__ unsigned long long g_prof[24];
 #define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
 #define PROF_ACC(cat)                                                              \
     do {                                                                           \
         unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
-        if (threadIdx.x == 0 && blockIdx.x == 0) atomicAdd(&g_prof[cat], _t1 - _pt); \
+        if (threadIdx.x == 0) atomicAdd(&g_prof[cat], _t1 - _pt);                   \
         _pt = _t1;                                                                 \
     } while (0)
 #else
@@ -182,7 +183,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     return f;
 }
 
-template <bool HG, bool VG, int RM>
+template <bool HG, bool VG, int RM, int OCC>
 struct Lay {
     static constexpr int RMAX = RM;   // row slots of the triangular solves (n <= 64 RM)
     using HT = typename std::conditional<HG, gdouble, ldouble>::type;
@@ -195,10 +196,10 @@ struct Lay {
     VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
 };
 
-template <bool HG, bool VG, int RM>
-__device__ __forceinline__ Lay<HG, VG, RM> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
+template <bool HG, bool VG, int RM, int OCC>
+__device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
                                                     int O, int Hb) {
-    Lay<HG, VG, RM> L;
+    Lay<HG, VG, RM, OCC> L;
     L.V = V; L.O = O; L.Hb = Hb; L.N = V * Hb; L.n = L.N + 1;
     L.mp = V * (V - 1) / 2 * Hb;
     L.m = L.mp + V * O * Hb;
@@ -213,7 +214,7 @@ __device__ __forceinline__ Lay<HG, VG, RM> make_lay(ldouble* lds, gdouble* ws, c
     L.scr = lds + f.scr; L.Wt = lds + f.Wt;
     L.rinfo = (lint*)(lds + f.rinfo);
     if constexpr (HG) L.H = ws + f.H; else L.H = lds + f.H;
-    typename Lay<HG, VG, RM>::VT* vb;
+    typename Lay<HG, VG, RM, OCC>::VT* vb;
     if constexpr (VG) vb = ws + f.vec; else vb = lds + f.vec;
     const int st = f.mcAlloc;
     L.s = vb; L.lam = vb + st; L.ds = vb + 2 * st; L.dl = vb + 3 * st; L.rp = vb + 4 * st;
@@ -665,12 +666,12 @@ __device__ int setup_problem(const cKArgs& a, const DevParams& P, const LT& L, i
 
 // Out-of-line setup: the trigonometry and expm constants stay out of the
 // register allocation of the solve loop.
-template <bool HG, bool VG, int RM>
+template <bool HG, bool VG, int RM, int OCC>
 __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int b, int Hb) {
     const cKArgs& a = *ap;
     const DevParams& P = *a.P;
     const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
-    const Lay<HG, VG, RM> L = make_lay<HG, VG, RM>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
+    const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
 }
 
@@ -887,15 +888,24 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
 
 // ---------------------------------------------------------------------------
 // Factorisation  K = L D L'  (L unit lower, stored strictly below the
-// diagonal of H; dvec = D, dinv = 1/D), blocked right-looking, panel width CB:
-//   1. wave 0 factors the n x CB panel in registers (pivots and panel-row
-//      entries broadcast with v_readlane: no barrier inside the panel);
-//   2. all 256 threads apply the rank-CB trailing update
-//      H_ik -= sum_c L_ic D_c L_kc in 2x2 register tiles with 16-byte loads.
-// Two barriers per panel, no square roots.  Returns false on a non-positive
-// pivot (K not numerically positive definite).
+// diagonal of H; dinv = 1/D), blocked right-looking, panel width CB, with a
+// one-panel look-ahead.  Per panel step (one barrier):
+//   * wave 0 applies the current panel's rank-CB update to the NEXT panel's
+//     columns and factors that panel in registers (pivots and panel-row
+//     entries broadcast with v_readlane: no barrier inside the panel);
+//   * waves 1.. apply the current panel's update to the columns beyond the
+//     next panel, H_ik -= sum_c L_ic D_c L_kc, in 2x2 register tiles with
+//     16-byte loads.
+// The serial panel chain of wave 0 thus runs concurrently with the trailing
+// update instead of between two barriers.  Pivots and the failure flag are
+// double-buffered by panel parity.  Returns false on a non-positive pivot
+// (K not numerically positive definite).
 // ---------------------------------------------------------------------------
-#define CB 8
+#ifndef SCPQP_CB
+#define SCPQP_CB 8
+#endif
+#define CB SCPQP_CB
+static_assert(CB % 2 == 0 && CB <= 8, "pivot double buffer holds 2 x 8 entries");
 
 // 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
 // a fraction of the IEEE division sequence's latency on the serial panel path).
@@ -911,123 +921,176 @@ __device__ __forceinline__ bool wave0() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;   // wave-uniform branch
 }
 
+// Wave 0: factor the panel of columns [r0, r0 + jb) in registers, rows
+// i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB
+// update of the previous panel (columns [jp, jp + CB), pivots dprev).
+// Branch-free: rows >= n read a clamped row, columns >= jb of the last panel
+// are padded with an identity block (D = 1, no coupling), and entries above
+// the diagonal (lane < c) only hold values that are never broadcast or stored.
+template <int RS, class HP>
+__device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
+                                             const ldouble* dprev, ldouble* dout, lint* flag) {
+    const int lane = threadIdx.x & 63;
+    double p[RS][CB];
+    int ro[RS];
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+        ro[t] = roff(i < n ? i : n - 1);
+#pragma unroll
+        for (int c = 0; c < CB; c += 2) {
+            const double2v v = ld2(H + ro[t] + r0 + c);
+            p[t][c] = v.x;
+            p[t][c + 1] = v.y;
+        }
+    }
+    if (jp >= 0) {
+        // look-ahead update: p_ic -= sum_c' (L_ic' D_c') L_{r0+c, c'}
+        double li[RS][CB];
+#pragma unroll
+        for (int t = 0; t < RS; ++t)
+#pragma unroll
+            for (int c = 0; c < CB; c += 2) {
+                const double2v v = ld2(H + ro[t] + jp + c);
+                li[t][c] = v.x * dprev[c];
+                li[t][c + 1] = v.y * dprev[c + 1];
+            }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            // one broadcast row in flight at a time (keeps the panel within the
+            // register budget of 3 workgroups per CU)
+            asm volatile("" ::: "memory");
+            const int kr = r0 + c < n ? r0 + c : n - 1;
+            const int ko = roff(kr) + jp;
+            double lk[CB];
+#pragma unroll
+            for (int c2 = 0; c2 < CB; c2 += 2) {
+                const double2v v = ld2(H + ko + c2);
+                lk[c2] = v.x;
+                lk[c2 + 1] = v.y;
+            }
+#pragma unroll
+            for (int t = 0; t < RS; ++t) {
+                double sacc = 0.0;
+#pragma unroll
+                for (int c2 = 0; c2 < CB; c2 += 2) sacc += li[t][c2] * lk[c2] + li[t][c2 + 1] * lk[c2 + 1];
+                p[t][c] -= sacc;
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+            p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
+    }
+    int bad = 0;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        const double D = readlane_d(p[0][c], c);
+        bad |= !(D > 0.0) || !isfinite(D);
+        const double inv = recip(D);
+#pragma unroll
+        for (int c2 = c + 1; c2 < CB; ++c2) {
+            const double lc = readlane_d(p[0][c], c2) * inv;
+#pragma unroll
+            for (int t = 0; t < RS; ++t) p[t][c2] -= p[t][c] * lc;
+        }
+#pragma unroll
+        for (int t = 0; t < RS; ++t) p[t][c] *= inv;
+        if (lane == 0 && c < jb) {
+            dinv[r0 + c] = inv;
+            dout[c] = D;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+        if (i < n) {
+#pragma unroll
+            for (int c = 0; c < CB; ++c)
+                if (c < jb && c <= lane + 64 * t) H[ro[t] + r0 + c] = p[t][c];
+        }
+    }
+    if (lane == 0) flag[0] = bad;
+}
+
+// Rank-CB update of panel j0 (pivots dcur) on rows/columns >= r1, by threads
+// [t0, t0 + nth) of the workgroup.  2x2 tiles (ti >= tk) enumerated linearly
+// so every thread gets ceil(ntile / nth) tiles; two tiles per pass so their
+// LDS latencies overlap.  r1 is even, so the (i0, i0 + 1) element of a
+// diagonal tile is row i0's padding slot, and row n (i1 == n) is the spare
+// row the plan allocates: the tile stores need no predicates.
+template <class HP>
+__device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, const ldouble* dcur,
+                                                int t0, int nth) {
+    double dc[CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c) dc[c] = dcur[c];
+    const int T = (n - r1 + 1) >> 1;
+    const int ntile = T * (T + 1) / 2;
+    for (int t = t0; t < ntile; t += 2 * nth) {
+        const int tb = t + nth < ntile ? t + nth : t;
+        int ia[2], ka[2];
+        tri_decode(t, ia[0], ka[0]);
+        tri_decode(tb, ia[1], ka[1]);
+        double sm[2][4];
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+            const int o0 = roff(r1 + 2 * ia[u2]), o1 = roff(r1 + 2 * ia[u2] + 1);
+            const int q0 = roff(r1 + 2 * ka[u2]), q1 = roff(r1 + 2 * ka[u2] + 1);
+            double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
+#pragma unroll
+            for (int c = 0; c < CB; c += 2) {
+                const double2v x0 = ld2(H + o0 + j0 + c), x1 = ld2(H + o1 + j0 + c);
+                const double2v y0 = ld2(H + q0 + j0 + c), y1 = ld2(H + q1 + j0 + c);
+                const double e0 = x0.x * dc[c], e1 = x0.y * dc[c + 1];
+                const double f0 = x1.x * dc[c], f1 = x1.y * dc[c + 1];
+                s00 += e0 * y0.x + e1 * y0.y;
+                s01 += e0 * y1.x + e1 * y1.y;
+                s10 += f0 * y0.x + f1 * y0.y;
+                s11 += f0 * y1.x + f1 * y1.y;
+            }
+            sm[u2][0] = s00; sm[u2][1] = s01; sm[u2][2] = s10; sm[u2][3] = s11;
+        }
+#pragma unroll
+        for (int u2 = 0; u2 < 2; ++u2) {
+            if (u2 == 1 && tb == t) break;
+            const int i0 = r1 + 2 * ia[u2], k0 = r1 + 2 * ka[u2];
+            const int o0 = roff(i0), o1 = roff(i0 + 1);
+            H[o0 + k0] -= sm[u2][0];
+            H[o0 + k0 + 1] -= sm[u2][1];
+            H[o1 + k0] -= sm[u2][2];
+            H[o1 + k0 + 1] -= sm[u2][3];
+        }
+    }
+}
+
 template <class LT>
 __device__ bool cholesky(const LT& L) {
-    const int tid = threadIdx.x;
     const int n = __builtin_amdgcn_readfirstlane(L.n);
-    const int ty = tid / TXD, tx = tid % TXD;
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
-    lint* flag = (lint*)(L.red + 120);
-    ldouble* dvec = L.red + 64;   // pivots of the current panel (CB)
+    lint* flag = (lint*)(L.red + 120);   // [parity]
+    ldouble* dbuf = L.red + 64;          // pivots [parity][CB]
     PROF_T0();
-    for (int j0 = 0; j0 < n; j0 += CB) {
-        const int jb = min(CB, n - j0);
+    for (int r0 = 0, par = 0; r0 < n; r0 += CB, par ^= 1) {
+        const int jp = r0 - CB;   // previous panel (none at the first step)
+        const int jb = min(CB, n - r0), r1 = r0 + jb;
+        const ldouble* dprev = dbuf + (par ^ 1) * CB;
         if (wave0()) {
-            // Panel in registers, rows i = j0 + lane + 64 t.  Branch-free: rows
-            // >= n load zeros, columns >= jb of the last panel are padded with an
-            // identity block (D = 1, no coupling), and updates of entries above
-            // the diagonal (lane < c2) only touch values that are never broadcast
-            // or stored.
-            const int lane = tid;
-            double p[RS][CB];
-#pragma unroll
-            for (int t = 0; t < RS; ++t) {
-                const int i = j0 + lane + 64 * t;
-                const int ir = i < n ? i : n - 1;
-#pragma unroll
-                for (int c = 0; c < CB; c += 2) {
-                    const double2v v = ld2(L.H + roff(ir) + j0 + c);
-                    p[t][c] = (i < n && c < jb) ? v.x : ((t == 0 && lane == c) ? 1.0 : 0.0);
-                    p[t][c + 1] =
-                        (i < n && c + 1 < jb) ? v.y : ((t == 0 && lane == c + 1) ? 1.0 : 0.0);
-                }
-            }
-            int bad = 0;
-#pragma unroll
-            for (int c = 0; c < CB; ++c) {
-                const double D = readlane_d(p[0][c], c);
-                bad |= !(D > 0.0) || !isfinite(D);
-                const double inv = recip(D);
-#pragma unroll
-                for (int c2 = c + 1; c2 < CB; ++c2) {
-                    const double lc = readlane_d(p[0][c], c2) * inv;
-#pragma unroll
-                    for (int t = 0; t < RS; ++t) p[t][c2] -= p[t][c] * lc;
-                }
-#pragma unroll
-                for (int t = 0; t < RS; ++t) p[t][c] *= inv;
-                if (lane == 0 && c < jb) {
-                    L.dinv[j0 + c] = inv;
-                    dvec[c] = D;
-                }
-            }
-#pragma unroll
-            for (int t = 0; t < RS; ++t) {
-                const int i = j0 + lane + 64 * t;
-                if (i < n) {
-#pragma unroll
-                    for (int c = 0; c < CB; ++c)
-                        if (c < jb && c <= lane + 64 * t) L.H[roff(i) + j0 + c] = p[t][c];
-                }
-            }
-            if (lane == 0) flag[0] = bad;
+            // rows r0 .. n-1 only: once they fit one slot per lane the panel
+            // runs with one register row (half the VALU work of the chain)
+            ldouble* dn = dbuf + par * CB;
+            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
+            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
+        } else if (jp >= 0 && r1 < n) {
+            trailing_update(L.H, n, jp, r1, dprev, (int)threadIdx.x - 64, NT - 64);
         }
         __syncthreads();
-        PROF_ACC(12);
-        if (flag[0]) return false;
-        // Rank-CB trailing update H_ik -= sum_c L_ic D_c L_kc in 2x2 register
-        // tiles.  r0 is even, so the (i0, i0 + 1) element of a diagonal tile is
-        // row i0's padding slot, and row n (i1 == n) is the spare row the plan
-        // allocates: the tile stores need no predicates.
-        const int r0 = j0 + jb;
-        if (r0 < n) {
-            double dc[CB];
-#pragma unroll
-            for (int c = 0; c < CB; ++c) dc[c] = dvec[c];
-            // 2x2 tiles (ti >= tk) enumerated linearly so every thread gets
-            // ceil(ntile / NT) tiles (no triangular imbalance); two tiles per
-            // pass so their LDS latencies overlap.
-            const int T = (n - r0 + 1) >> 1;
-            const int ntile = T * (T + 1) / 2;
-            for (int t = tid; t < ntile; t += 2 * NT) {
-                const int tb = t + NT < ntile ? t + NT : t;
-                int ia[2], ka[2];
-                tri_decode(t, ia[0], ka[0]);
-                tri_decode(tb, ia[1], ka[1]);
-                double sm[2][4];
-#pragma unroll
-                for (int u2 = 0; u2 < 2; ++u2) {
-                    const int o0 = roff(r0 + 2 * ia[u2]), o1 = roff(r0 + 2 * ia[u2] + 1);
-                    const int q0 = roff(r0 + 2 * ka[u2]), q1 = roff(r0 + 2 * ka[u2] + 1);
-                    double s00 = 0.0, s01 = 0.0, s10 = 0.0, s11 = 0.0;
-#pragma unroll
-                    for (int c = 0; c < CB; c += 2) {
-                        const double2v x0 = ld2(L.H + o0 + j0 + c), x1 = ld2(L.H + o1 + j0 + c);
-                        const double2v y0 = ld2(L.H + q0 + j0 + c), y1 = ld2(L.H + q1 + j0 + c);
-                        const double e0 = x0.x * dc[c], e1 = x0.y * dc[c + 1];
-                        const double f0 = x1.x * dc[c], f1 = x1.y * dc[c + 1];
-                        s00 += e0 * y0.x + e1 * y0.y;
-                        s01 += e0 * y1.x + e1 * y1.y;
-                        s10 += f0 * y0.x + f1 * y0.y;
-                        s11 += f0 * y1.x + f1 * y1.y;
-                    }
-                    sm[u2][0] = s00; sm[u2][1] = s01; sm[u2][2] = s10; sm[u2][3] = s11;
-                }
-#pragma unroll
-                for (int u2 = 0; u2 < 2; ++u2) {
-                    if (u2 == 1 && tb == t) break;
-                    const int i0 = r0 + 2 * ia[u2], k0 = r0 + 2 * ka[u2];
-                    const int o0 = roff(i0), o1 = roff(i0 + 1);
-                    L.H[o0 + k0] -= sm[u2][0];
-                    L.H[o0 + k0 + 1] -= sm[u2][1];
-                    L.H[o1 + k0] -= sm[u2][2];
-                    L.H[o1 + k0 + 1] -= sm[u2][3];
-                }
-            }
-        }
-        __syncthreads();
-        PROF_ACC(13);
+        if (flag[par]) return false;
     }
+    PROF_ACC(13);
     return true;
 }
 
@@ -1416,17 +1479,17 @@ struct D4 {
     double a, b, c, d;
 };
 
-template <bool HG, bool VG, int RM>
-__device__ __forceinline__ Lay<HG, VG, RM> lay_of(const Ctx& c) {
+template <bool HG, bool VG, int RM, int OCC>
+__device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
     const Off f = plan_offsets(c.P->nV, c.P->nO, c.P->hpMax, HG, VG);
-    return make_lay<HG, VG, RM>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
+    return make_lay<HG, VG, RM, OCC>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
 }
-#define PHASE template <bool HG, bool VG, int RM> __device__ __noinline__
+#define PHASE template <bool HG, bool VG, int RM, int OCC> __device__ __noinline__
 #define LAYDEF                  \
     const DevParams& P = *c.P;  \
-    const Lay<HG, VG, RM> L = lay_of<HG, VG, RM>(c); \
+    const Lay<HG, VG, RM, OCC> L = lay_of<HG, VG, RM, OCC>(c); \
     (void)P
-#define PH(f) f<HG, VG, RM>
+#define PH(f) f<HG, VG, RM, OCC>
 
 PHASE void ph_assemble(Ctx c, double rho) {
     LAYDEF;
@@ -1597,13 +1660,22 @@ PHASE void ph_polish_tv(Ctx c) {
     __syncthreads();
 }
 // rp = G x_k - h;  y += rp / delta on the active set.  Returns
-// {max |x_k - x_{k-1}|, max |x_k|} (x_{k-1} kept in rd, dead during the polish).
+// {max |x_k - x_{k-1}|, max |x_k|, max rp over the inactive rows, -min y over
+// the active rows} (x_{k-1} kept in rd, dead during the polish).
 PHASE D4 ph_polish_dual(Ctx c) {
     LAYDEF;
     const double idl = 1.0 / P.polDelta;
     g_apply(L, L.dz, L.rp, true);
-    for (int r = threadIdx.x; r < L.mc; r += NT)
-        if (L.sa[r] != 0.0) L.la[r] += L.rp[r] * idl;
+    double viol = -1e300, yneg = -1e300;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        if (L.sa[r] != 0.0) {
+            const double y = L.la[r] + L.rp[r] * idl;
+            L.la[r] = y;
+            yneg = fmax(yneg, -y);
+        } else {
+            viol = fmax(viol, L.rp[r]);
+        }
+    }
     double dmax = 0.0, xmax = 0.0;
     for (int e = threadIdx.x; e < L.n; e += NT) {
         const double x = L.dz[e];
@@ -1611,9 +1683,9 @@ PHASE D4 ph_polish_dual(Ctx c) {
         xmax = fmax(xmax, fabs(x));
         L.rd[e] = x;
     }
-    double red[4] = {dmax, xmax, 0.0, 0.0};
-    block_reduce4<2>(red, 3, L.red);
-    return D4{red[0], red[1], 0.0, 0.0};
+    double red[4] = {dmax, xmax, viol, yneg};
+    block_reduce4<4>(red, 15, L.red);
+    return D4{red[0], red[1], red[2], red[3]};
 }
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
 // Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
@@ -1672,9 +1744,14 @@ PHASE void ph_take_u(Ctx c) {
 // warm start may take before the IPM runs, and the multiplier iteration's
 // convergence test (oracle POLISH_TOL).
 constexpr int kPolishRounds = 6;
-constexpr int kWarmRounds = 3;
+constexpr int kWarmRounds = 8;
 constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: P.nRefine)
 constexpr double kPolishTol = 1e-10;
+// Warm rounds stop refining as soon as the iterate shows the active set is
+// wrong (an inactive row violated, or an active multiplier negative, by more
+// than this in scaled units): the correction comes earlier and the refinement
+// spent on a wrong active set is skipped.
+constexpr double kWarmEarly = 1e-6;
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
@@ -1688,9 +1765,9 @@ struct QpStats {
 // refined until x stops moving (|dx| <= kPolishTol max(1, |x|), at most
 // P.nRefine solves per round), certified, else the active set is corrected
 // (primal-dual active set) and the round repeats.  Returns true if certified.
-template <bool HG, bool VG, int RM>
+template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds, int cap,
-                                              QpStats& st) {
+                                              double early, QpStats& st) {
     const DevParams& P = *c.P;
     bool ok = false, refactor = true, extended = false;
     PROF_T0();
@@ -1713,6 +1790,7 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds
                 conv = 1;
                 break;
             }
+            if (ref >= 1 && (d.c > early || d.d > early)) break;
         }
         const int acc = PH(ph_polish_accept)(c, hmax, conv);
         PROF_ACC(8);
@@ -1730,7 +1808,7 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds
 // One convexified QP.  warm: try the previous QP's active set first (a few
 // polish rounds, no interior point iterations); on failure, or cold, run the
 // Mehrotra IPM from the CVXOPT initial point and polish its active set.
-template <bool HG, bool VG, int RM>
+template <bool HG, bool VG, int RM, int OCC>
 __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st) {
     const DevParams& P = *c.P;
     const int mc = (P.nV * (P.nV - 1) / 2 + P.nV * P.nO) * c.Hb + 2 * P.nV * c.Hb + 1;
@@ -1738,22 +1816,23 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
     const double hmax = sc.a, qmax = sc.b;
     if (warm) {
         PH(ph_polish_warm)(c);
-        if (polish_rounds<HG, VG, RM>(c, hmax, kWarmRounds, kWarmRefine, st)) {
+        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, kWarmRounds, kWarmRefine, kWarmEarly, st)) {
             ++st.warm_ok;
             return true;
         }
     }
     // ---- initial point (CVXOPT coneqp): (P + G'G) x = -q + G'h;  s = h - Gx;  lam = -s; shift
+    PROF_T0();
     PH(ph_init_a)(c);
     PH(ph_assemble)(c, 0.0);
     PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
     PH(ph_rhs_from_tv)(c, 0.0);
     PH(ph_solve)(c, 0);
     PH(ph_init_b)(c);
+    PROF_ACC(16);
     // ---- Mehrotra iterations
     int it = 0;
     bool conv = false;
-    PROF_T0();
     for (; it < P.maxIpm; ++it) {
         PROF_ACC(0);
         const D4 res = PH(ph_residuals)(c);
@@ -1787,7 +1866,7 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
     if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
     // ---- active-set polish on {lam > s}
     PH(ph_polish_prep)(c);
-    const bool ok = polish_rounds<HG, VG, RM>(c, hmax, kPolishRounds, P.nRefine, st);
+    const bool ok = polish_rounds<HG, VG, RM, OCC>(c, hmax, kPolishRounds, P.nRefine, INFINITY, st);
     if (!ok) *qflags |= SCPQP_FL_POLISH_REJECTED;
     return ok;
 }
@@ -1795,8 +1874,8 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
-template <bool HG, bool VG, int RM>
-__global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
+template <bool HG, bool VG, int RM, int OCC>
+__global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     ldouble* smem = (ldouble*)smem_;
     const DevParams& P = *a.P;
     const int tid = threadIdx.x;
@@ -1833,7 +1912,7 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
         const Ctx c{a.P, ws, Hb};
         const int V = P.nV, N = V * Hb, O = P.nO;
         PROF_T0();
-        const int sflag = setup_problem_ni<HG, VG, RM>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
+        const int sflag = setup_problem_ni<HG, VG, RM, OCC>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
         PROF_ACC(10);
         const int sflag_any = __syncthreads_or(sflag);
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
@@ -1901,9 +1980,13 @@ __global__ __launch_bounds__(NT, 2) void scp_kernel(KArgs a) {
 #endif
             PH(ph_linearise)(c);
             PROF_ACC(11);
-            prev_ok = qp_solve<HG, VG, RM>(c, &qflags, warm_on && prev_ok, qs);
+            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_on && prev_ok, qs);
+#ifdef SCPQP_PROF
+            _pt = __builtin_amdgcn_s_memtime();
+#endif
             PH(ph_take_u)(c);
             ev = PH(ph_evaluate)(c, nullptr, nullptr);
+            PROF_ACC(17);
             const double delta = (obj0 + P.slackW * mv0) - (ev.obj + P.slackW * ev.maxv);
             obj0 = ev.obj;
             mv0 = ev.maxv;
@@ -1973,7 +2056,7 @@ struct scpqp_handle {
     int* counter = nullptr;
     double* ws = nullptr;
     size_t wsBytes = 0;
-    int hG = 0, vG = 0;
+    int hG = 0, vG = 0, occ = 2;
     size_t ldsBytes = 0;
     long long wsStride = 0;
     int grid = 0;
@@ -1985,28 +2068,39 @@ const size_t kLdsLimit = 163840;
 
 int plan(scpqp_handle* h) {
     const int V = h->dims.n_veh, O = h->dims.n_obst, Hm = h->dims.hp_max;
-    for (int cfg = 0; cfg < 3; ++cfg) {
-        const bool hG = cfg >= 2, vG = cfg >= 1;
-        const Off f = plan_offsets(V, O, Hm, hG, vG);
+    // Plans: 0 everything in LDS, 1 constraint vectors in the workspace, 2 also
+    // the KKT matrix.  Take the plan that fits the most workgroups per CU (the
+    // kernel is latency-bound: co-resident problems hide each other's waits);
+    // on a tie the one with less in global memory.  The register budget is
+    // compiled for 2 or 3 workgroups per CU (OCC).
+    const char* force = getenv("SCPQP_PLAN");   // diagnostic: force a plan
+    const int cfg0 = force ? atoi(force) : 0, cfg1 = force ? cfg0 + 1 : 3;
+    int best = -1, bestPer = 0;
+    for (int cfg = cfg0; cfg < cfg1 && cfg < 3; ++cfg) {
+        const Off f = plan_offsets(V, O, Hm, cfg >= 2, cfg >= 1);
         const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
-        if (lds <= kLdsLimit) {
-            h->hG = hG;
-            h->vG = vG;
-            h->ldsBytes = lds;
-            h->wsStride = f.ws;
-            int perCU = (int)(kLdsLimit / lds);
-            if (perCU > 8) perCU = 8;
-            if (perCU < 1) perCU = 1;
-            h->grid = h->cus * perCU;
-            return 0;
+        if (lds > kLdsLimit) continue;
+        int perCU = (int)(kLdsLimit / lds);
+        if (perCU > 3) perCU = 3;   // beyond 3 the register budget, not LDS, bounds residency
+        if (perCU > bestPer) {
+            best = cfg;
+            bestPer = perCU;
         }
     }
-    return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
+    if (best < 0) return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
+    const Off f = plan_offsets(V, O, Hm, best >= 2, best >= 1);
+    h->hG = best >= 2;
+    h->vG = best >= 1;
+    h->ldsBytes = (size_t)(f.persist + f.uni) * sizeof(double);
+    h->wsStride = f.ws;
+    h->grid = h->cus * bestPer;
+    h->occ = bestPer >= 3 ? 3 : 2;
+    return 0;
 }
 
-template <bool HG, bool VG, int RM>
+template <bool HG, bool VG, int RM, int OCC>
 int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
-    auto kern = scp_kernel<HG, VG, RM>;
+    auto kern = scp_kernel<HG, VG, RM, OCC>;
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->ldsBytes));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), h->ldsBytes, st, a);
@@ -2033,12 +2127,17 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
+    const int occ = h->occ;   // workgroups per CU the register budget is compiled for
 #define SCPQP_DISPATCH(HGV, VGV)                                              \
-    switch (R) {                                                             \
-        case 1: return launch_t<HGV, VGV, 1>(h, a, st, grid);                \
-        case 2: return launch_t<HGV, VGV, 2>(h, a, st, grid);                \
-        case 3: return launch_t<HGV, VGV, 3>(h, a, st, grid);                \
-        default: return launch_t<HGV, VGV, 4>(h, a, st, grid);               \
+    switch (R * 4 + occ) {                                                   \
+        case 6: return launch_t<HGV, VGV, 1, 2>(h, a, st, grid);             \
+        case 7: return launch_t<HGV, VGV, 1, 3>(h, a, st, grid);             \
+        case 10: return launch_t<HGV, VGV, 2, 2>(h, a, st, grid);            \
+        case 11: return launch_t<HGV, VGV, 2, 3>(h, a, st, grid);            \
+        case 14: return launch_t<HGV, VGV, 3, 2>(h, a, st, grid);            \
+        case 15: return launch_t<HGV, VGV, 3, 3>(h, a, st, grid);            \
+        case 19: return launch_t<HGV, VGV, 4, 3>(h, a, st, grid);            \
+        default: return launch_t<HGV, VGV, 4, 2>(h, a, st, grid);            \
     }
     if (h->hG) { SCPQP_DISPATCH(true, true) }
     if (h->vG) { SCPQP_DISPATCH(false, true) }
@@ -2240,9 +2339,9 @@ int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in,
 
 #ifdef SCPQP_PROF
 int scpqp_prof_read(unsigned long long* out, int reset) {
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24));
     if (reset) {
-        unsigned long long z[16] = {0};
+        unsigned long long z[24] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
     }
     return 0;

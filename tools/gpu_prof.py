@@ -1,4 +1,4 @@
-"""Phase-stamp breakdown (diagnostic build libscpqp_prof.so): cycles of workgroup 0."""
+"""Phase-stamp breakdown (diagnostic build libscpqp_prof.so): cycles summed over all workgroups."""
 import os, sys, ctypes as C, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -14,20 +14,22 @@ from scpqp import batch as BT
 from scpqp.solver import ScpQpSolver
 names = ["ipm-loop-top", "residuals", "assemble", "cholesky", "newton(pred)", "maxstep+corr",
          "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
-         "chol:panel", "chol:update", "solve:fwd", "solve:bwd"]   # 12-15: sub-phases of 3 / 9
-for nv, hp, B in [(4, 20, 1), (8, 30, 1)]:
+         "chol:panel0", "chol:steps", "solve:fwd", "solve:bwd",   # 12-15: sub-phases of 3 / 9
+         "ipm-init", "take_u+evaluate"]
+for nv, hp, B in [(4, 20, 1), (4, 20, 1024), (8, 30, 1)]:
     sc = R.circle_scenario(nv, Hp=hp)
     bt = BT.make_batch(sc, B, base_seed=1000)
     S = ScpQpSolver(sc, max_batch=B)
     S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 16)()
+    buf = (C.c_ulonglong * 24)()
     lib.scpqp_prof_read(buf, 1)
     t = time.time()
     out = S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
     wall = time.time() - t
     lib.scpqp_prof_read(buf, 1)
-    tot = sum(buf[i] for i in range(12) if i != 9)
-    nipm = out.n_ipm[0].item()
-    print(f"nv={nv} hp={hp}: wall {wall*1e3:.2f} ms, nscp {out.n_scp[0].item()} nipm {nipm}")
+    tot = sum(buf[i] for i in list(range(12)) + [16, 17])
+    nipm = out.n_ipm.sum().item()
+    print(f"nv={nv} hp={hp} B={B}: wall {wall*1e3:.2f} ms, nscp {out.n_scp.sum().item()} nipm {nipm} "
+          f"warm {out.n_warm.sum().item()} refine {out.n_refine.sum().item()} total {tot} cyc")
     for i, nme in enumerate(names):  # 12-15 are sub-phases (already inside 3 and 9)
-        print(f"   {nme:15s} {buf[i]:12d} cyc  {buf[i]/max(nipm,1):10.0f}/ipm-it")
+        print(f"   {nme:15s} {buf[i]:12d} cyc  {buf[i]/max(nipm,1):10.0f}/ipm-it  {100.0*buf[i]/tot:5.1f}%")
