@@ -59,6 +59,7 @@ namespace {
 // Diagnostic phase stamps (built only with -DSCPQP_PROF; never in the shipped kernel).
 #ifdef SCPQP_PROF
 __device__ unsigned long long g_prof[24];
+__device__ unsigned long long g_ptime[8192 * 2];   // per-problem [start, end] (100 MHz realtime)
 #define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
 #define PROF_ACC(cat)                                                              \
     do {                                                                           \
@@ -1104,7 +1105,10 @@ __device__ bool cholesky(const LT& L) {
 
 template <int R, class HP>
 struct Solver {
-    static constexpr int SCH = 4;   // chunk (columns / rows) streamed per step group
+#ifndef SCPQP_SCH
+#define SCPQP_SCH 4
+#endif
+    static constexpr int SCH = SCPQP_SCH;   // chunk (columns / rows) streamed per step group
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
     int lane, n, ld;
@@ -1911,6 +1915,9 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
         }
         const Ctx c{a.P, ws, Hb};
         const int V = P.nV, N = V * Hb, O = P.nO;
+#ifdef SCPQP_PROF
+        if (tid == 0 && b < 8192) g_ptime[2 * b] = __builtin_amdgcn_s_memrealtime();
+#endif
         PROF_T0();
         const int sflag = setup_problem_ni<HG, VG, RM, OCC>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
         PROF_ACC(10);
@@ -1980,7 +1987,10 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
 #endif
             PH(ph_linearise)(c);
             PROF_ACC(11);
-            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_on && prev_ok, qs);
+            // warm start from the previous QP's active set from the third QP on: the
+            // first re-linearisation moves the active set too far for a few
+            // active-set corrections to recover it (tools/polish_study.py: 0/16)
+            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_on && prev_ok && it >= 2, qs);
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
@@ -2020,6 +2030,9 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             if (a.npol) a.npol[b] = qs.rounds;
             if (a.nref) a.nref[b] = qs.refine;
             if (a.nwarm) a.nwarm[b] = qs.warm_ok;
+#ifdef SCPQP_PROF
+            if (b < 8192) g_ptime[2 * b + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
             if (a.obj) a.obj[b] = ev.obj;
             if (a.maxv) a.maxv[b] = ev.maxv;
             if (a.sumv) a.sumv[b] = ev.sumv;
@@ -2338,6 +2351,10 @@ int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in,
 }
 
 #ifdef SCPQP_PROF
+int scpqp_prof_times(unsigned long long* out, int n) {
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptime), sizeof(unsigned long long) * 2 * n));
+    return 0;
+}
 int scpqp_prof_read(unsigned long long* out, int reset) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24));
     if (reset) {

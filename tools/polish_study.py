@@ -116,7 +116,12 @@ def main():
         for ct, v in COARSE.items():
             v = np.array(v, float)
             print(f'   ipm tol {ct:.0e}: ipm its {v[:,1].mean():.2f} (full {v[:,0].mean():.2f}) polish ok {int(v[:,2].sum())}/{len(v)} solves {v[:,3].mean():.2f} rounds {v[:,4].mean():.2f} max rounds {v[:,4].max():.0f}')
-        for t in []: print('   prob %d qp %d/%d ok %s solves %d |A_prev| %d |A| %d diff %d' % t)
+        import collections
+        agg = collections.defaultdict(lambda: [0, 0, 0])
+        for t in TRACE:
+            a = agg[min(t[1], 5)]; a[0] += 1; a[1] += int(t[3]); a[2] += t[4]
+        for k in sorted(agg):
+            a = agg[k]; print(f'   qp index {k}{"+" if k == 5 else ""}: warm ok {a[1]}/{a[0]}  solves/attempt {a[2] / a[0]:.1f}')
         hist = np.bincount(cold_s)
         print("   cold solves histogram", {i: int(c) for i, c in enumerate(hist) if c})
 
