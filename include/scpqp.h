@@ -179,6 +179,45 @@ int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in,
 int scpqp_resources(scpqp_handle* h, int64_t* lds_bytes, int64_t* ws_bytes_per_wg,
                     int32_t* big_mode, int32_t* grid);
 
+/* ------------------------------------------------------------------------
+ * The bicycle plant around the solve (csrc/plant.hip).  Handle-free; every
+ * array is a DEVICE pointer (float64, C-contiguous), calls are asynchronous
+ * on `stream`.  The reference integrates with scipy odeint / dopri5; these
+ * use fixed-step RK4 with steps of at most h_max seconds (2.5e-3 recommended:
+ * ~1e-11 from the exact flow, below the reference's 1e-8 tolerances).
+ * ---------------------------------------------------------------------- */
+typedef struct scpqp_plant_params {
+    int32_t n_veh;                 /* scenario.nVeh                       */
+    int32_t pad0;
+    double lf[SCPQP_MAX_VEH];      /* scenario.Lf (Model.py:26)           */
+    double lr[SCPQP_MAX_VEH];      /* scenario.Lr (Model.py:27)           */
+} scpqp_plant_params;
+
+/* IterClass delay compensation (MPC_Iter.py:24-33): integrate Model.ode from
+ * x_meas [B][n_veh][6] over linspace(0, horizon, n_out) with the constant
+ * steering command u_hold [B][n_veh] (= u_path[v, -1]).  noise [B][n_veh][2]
+ * (may be NULL): constant additive terms of dx[0], dx[1] (Model.py:84-86).
+ * x0_out [B][n_veh][6] = Y[-1]; traj_out [B][n_out][6][n_veh] (may be NULL)
+ * = MPC_delay_compensation_trajectory. */
+int scpqp_delay_compensate(const scpqp_plant_params* p, int32_t B, double horizon, int32_t n_out,
+                           const double* x_meas, const double* u_hold, const double* noise,
+                           double* x0_out, double* traj_out, double h_max, void* stream);
+
+/* Plant simulation of one MPC step (main.py:184-191): for every output tick
+ * k = 0..n_ticks the reference restarts dopri5 at t0 from x_start and
+ * integrates to t0 + k*tick with the constant control u_tick[b][v][k]
+ * (= controlPathFullRes[v, ceil(t_k / tick) + 1]).  x_start [B][n_veh][6],
+ * noise [B][n_veh][2] or NULL, x_path [B][n_veh][n_ticks+1][6]. */
+int scpqp_plant_step(const scpqp_plant_params* p, int32_t B, int32_t n_ticks, double tick,
+                     const double* x_start, const double* u_tick, const double* noise,
+                     double* x_path, double h_max, void* stream);
+
+/* Steering-limit enforcement (main.py:164-174), in place on the solver's
+ * vehicle-major controls u[b*ld + v*hp + j]: U[0] clamped to +-umax and to
+ * u0 +- du_lim, U[j] to +-umax and U[j-1] +- du_lim.  u0, umax: [B][n_veh]. */
+int scpqp_clip_controls(int32_t B, int32_t n_veh, int32_t hp, int32_t ld, double du_lim, double* u,
+                        const double* u0, const double* umax, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,187 @@
+"""CPU restatement of the plant around the SCP solve.
+
+TEST INFRASTRUCTURE ONLY — the product never imports this file; only
+``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` may.
+
+The reference integrates the bicycle model (Model.py:61-87) with scipy:
+
+* delay compensation, ``IterClass`` (MPC_Iter.py:24-33): ``scipy.integrate.
+  odeint(model.ode, x_measured[v], linspace(0, delay_x + dt + delay_u, 10),
+  args=(u_path[v, -1], Lf[v], Lr[v]))`` — LSODA at its default rtol = atol =
+  1.49012e-8;
+* the plant, ``Simulation.runsimulation`` (main.py:184-191): ``scipy.integrate.
+  ode(model.odes_).set_integrator('dopri5', atol=1e-8, rtol=1e-8)``, restarted
+  at t0 = i*dt for every output time of the step with the control value of that
+  tick;
+* steering-limit enforcement (main.py:164-174) and the control-path bookkeeping
+  with the actuator delay (main.py:101-117, 176-182).
+
+The scipy calls below are the reference's own third-party calls with the same
+arguments (scipy 1.15 here; the reference pins no version).  ``*_exact`` runs
+the same initial value problems at rtol = atol = 1e-13 (DOP853) as the
+integration-error-free truth the GPU's fixed-step RK4 is checked against.
+``is_noise`` is False in main.py:235, so the plant is deterministic.
+"""
+from __future__ import annotations
+
+import math
+import warnings
+
+import numpy as np
+import scipy.integrate
+
+from . import scp_reference as R
+
+DELAY_STEPS = 10                          # MPC_Iter.py:21
+LATERAL_ACC_LIMIT = 9.81 / 2              # Scenarios.py:48
+NX = 6
+
+
+def _ode(x, t, u_ref, Lf, Lr):
+    """Model.ode with odeint's f(x, t, *args) signature (Model.py:61-87)."""
+    return R.bicycle_rhs(x, u_ref, Lf, Lr)
+
+
+def _odes(t, x, u_ref, Lf, Lr):
+    """Model.odes_ with scipy.integrate.ode's f(t, x, *args) signature (Model.py:89-114)."""
+    return R.bicycle_rhs(x, u_ref, Lf, Lr)
+
+
+def delay_horizon(sc):
+    """delay_x + dt + delay_u (MPC_Iter.py:28)."""
+    return sc.delay_x + sc.dt + sc.delay_u
+
+
+def delay_compensate(sc, x_measured, u_hold, steps=DELAY_STEPS):
+    """MPC_Iter.py:24-33.  x_measured [nVeh, 6], u_hold [nVeh] (= u_path[:, -1])
+    -> x0 [nVeh, 6], u0 [nVeh], trajectory [steps, 6, nVeh]."""
+    nV = len(u_hold)
+    times = np.linspace(0, delay_horizon(sc), steps)
+    x0 = np.zeros((nV, NX))
+    traj = np.zeros((steps, NX, nV))
+    for v in range(nV):
+        Y = scipy.integrate.odeint(_ode, np.asarray(x_measured[v], float), times,
+                                   args=(float(u_hold[v]), sc.Lf[v], sc.Lr[v]))
+        x0[v] = Y[-1]
+        traj[:, :, v] = Y
+    return x0, np.asarray(u_hold, float).copy(), traj
+
+
+def delay_compensate_exact(sc, x_measured, u_hold, steps=DELAY_STEPS):
+    """The same initial value problem at rtol = atol = 1e-13 (DOP853)."""
+    nV = len(u_hold)
+    times = np.linspace(0, delay_horizon(sc), steps)
+    traj = np.zeros((steps, NX, nV))
+    for v in range(nV):
+        sol = scipy.integrate.solve_ivp(_odes, (0.0, times[-1]), np.asarray(x_measured[v], float),
+                                        method="DOP853", t_eval=times, rtol=1e-13, atol=1e-13,
+                                        args=(float(u_hold[v]), sc.Lf[v], sc.Lr[v]))
+        traj[:, :, v] = sol.y.T
+    return traj[-1].T.copy(), traj
+
+
+def plant_step(sc, v, x_start, t0, u_of_k):
+    """main.py:184-191 for vehicle v: ``model_step [ticks_per_sim + 1, 6]``;
+    output k restarts dopri5 at t0 and integrates to timelist[k] with the
+    constant control u_of_k[k]."""
+    K = sc.ticks_per_sim + 1
+    timelist = np.linspace(t0, t0 + sc.dt, K)
+    out = np.zeros((K, NX))
+    for k in range(K):
+        ode = scipy.integrate.ode(_odes).set_integrator("dopri5", atol=1e-8, rtol=1e-8)
+        ode.set_initial_value(np.asarray(x_start, float), t=t0).set_f_params(
+            float(u_of_k[k]), sc.Lf[v], sc.Lr[v])
+        with warnings.catch_warnings():   # k = 0 integrates over a zero span, as the reference does
+            warnings.simplefilter("ignore", UserWarning)
+            out[k] = ode.integrate(timelist[k])
+    return out
+
+
+def plant_step_exact(sc, v, x_start, t0, u_of_k):
+    """plant_step at rtol = atol = 1e-13 (DOP853)."""
+    K = sc.ticks_per_sim + 1
+    timelist = np.linspace(t0, t0 + sc.dt, K)
+    out = np.zeros((K, NX))
+    out[0] = x_start
+    for k in range(1, K):
+        sol = scipy.integrate.solve_ivp(_odes, (t0, timelist[k]), np.asarray(x_start, float),
+                                        method="DOP853", rtol=1e-13, atol=1e-13,
+                                        args=(float(u_of_k[k]), sc.Lf[v], sc.Lr[v]))
+        out[k] = sol.y[:, -1]
+    return out
+
+
+def clip_controls(U, u0, umax, du_lim):
+    """main.py:164-174 on U [Hp, nVeh] (a copy is returned)."""
+    U = np.array(U, float, copy=True)
+    Hp, nV = U.shape
+    for v in range(nV):
+        U[0, v] = min(U[0, v], umax[v])
+        U[0, v] = max(U[0, v], -umax[v])
+        U[0, v] = min(U[0, v], u0[v] + du_lim)
+        U[0, v] = max(U[0, v], u0[v] - du_lim)
+        for j in range(1, Hp):
+            U[j, v] = min(U[j, v], umax[v])
+            U[j, v] = max(U[j, v], -umax[v])
+            U[j, v] = min(U[j, v], U[j - 1, v] + du_lim)
+            U[j, v] = max(U[j, v], U[j - 1, v] - du_lim)
+    return U
+
+
+def steering_limit(sc, speed, v):
+    """main.py:105-108: min(mechanical limit, atan(a_lat,max * L / v^2))."""
+    dyn = math.atan(LATERAL_ACC_LIMIT * (sc.Lf[v] + sc.Lr[v]) / speed ** 2)
+    return min(sc.mechanicalSteeringLimit, dyn)
+
+
+def control_tick_index(sc, t):
+    """main.py:187: index of controlPathFullRes read for output time t."""
+    return min(sc.ticks_total, math.ceil(t / sc.tick_length) + 1)
+
+
+class ClosedLoop:
+    """Restatement of ``Simulation.runsimulation`` (main.py:98-206) for one
+    realisation with the SCP controller of ``scp_reference`` (structured mode).
+    ``x_init`` [nVeh, 6] replaces scenario.x0 (main.py:73-75)."""
+
+    def __init__(self, sc, x_init=None):
+        self.sc = sc
+        nV = sc.nVeh
+        self.du_lim = sc.mechanicalSteeringLimit * 2              # Scenarios.py:50
+        self.path = np.full((NX, nV, sc.ticks_total + 1), np.nan)
+        self.control = np.full((nV, sc.ticks_total + 1), np.nan)
+        x_init = np.array([sc.x0[v] for v in range(nV)]) if x_init is None else x_init
+        for v in range(nV):
+            self.path[:, v, 0] = x_init[v]
+            self.control[v, 0:sc.ticks_delay_u + sc.ticks_per_sim + 1] = sc.u0[v]
+        self.u_prev = None
+        self.records = []
+
+    def step(self, i):
+        sc = self.sc
+        nV, tps = sc.nVeh, sc.ticks_per_sim
+        tick_now = i * tps
+        tick_meas = max(0, tick_now - sc.ticks_delay_x)
+        tick_act = min(sc.ticks_total + 1, tick_now + 1 + sc.ticks_delay_u + tps)
+        umax = np.array([steering_limit(sc, self.path[3, v, tick_now], v) for v in range(nV)])
+        x_meas = self.path[:, :, tick_meas].T
+        n_path = sc.ticks_delay_x + tps + sc.ticks_delay_u
+        u_path = np.zeros((nV, n_path))
+        lo = max(sc.ticks_delay_x - tick_now, 0)
+        u_path[:, lo:lo + tick_act - 1 - tick_meas] = self.control[:, tick_meas + 1:tick_act]
+        x0, u0, dtraj = delay_compensate(sc, x_meas, u_path[:, -1])
+        p = R.make_problem(sc, x0, u0, np.zeros((nV, 2)), Hp=sc.Hp)
+        res = R.scp_solve(p, u_warm=self.u_prev, mode="structured")
+        self.u_prev = res.u.copy()
+        U = clip_controls(res.U, u0, umax, self.du_lim)
+        for v in range(nV):
+            sl = np.arange(i * tps + 1 + sc.ticks_delay_u + tps, (i + 1) * tps + 1 + sc.ticks_delay_u + tps)
+            sl[sl >= self.control.shape[1] - 1] = self.control.shape[1] - 1
+            self.control[v, sl] = U[0, v]
+            timelist = np.linspace(i * sc.dt, (i + 1) * sc.dt, tps + 1)
+            u_of_k = [self.control[v, control_tick_index(sc, t)] for t in timelist]
+            ms = plant_step(sc, v, self.path[:, v, tick_now], i * sc.dt, u_of_k)
+            self.path[:, v, tps * i + 1:tps * (i + 1) + 1] = ms[1:].T
+        self.records.append(dict(x0=x0, u0=u0, delay_traj=dtraj, umax=umax, U=U, traj=res.traj,
+                                 n_scp=res.n_scp, u=res.u))
+        return self.records[-1]

@@ -2,7 +2,8 @@
 
 ``IterClass``  per-MPC-step preprocessing (MPC_Iter.py:13-55): delay
                compensation by integrating the plant over delay_x + dt + delay_u
-               (host odeint, as the reference), reference sampling on the GPU
+               on the GPU (``scpqp_delay_compensate``, fixed-step RK4 in place
+               of the reference's odeint), reference sampling on the GPU
                (``scpqp_sample_reference``), constant-velocity obstacle
                prediction.
 ``MPCclass``   discretisation + prediction + cost matrices (MPC_Iter.py:59-149).
@@ -16,7 +17,6 @@
 from math import sqrt
 
 import numpy as np
-import scipy.integrate
 
 from Scenarios import Indices
 
@@ -31,17 +31,13 @@ def delay_compensate(scenario, x_measured, u_path):
     nV, nx, nu = scenario.nVeh, scenario.model.nx, scenario.model.nu
     horizon = scenario.delay_x + scenario.dt + scenario.delay_u
     assert u_path.shape[1] * scenario.tick_length - horizon < 1e-10
-    times = np.linspace(0, horizon, DELAY_STEPS)
-    x0 = np.zeros([nV, nx])
-    u0 = np.zeros([nV, nu])
-    traj = np.zeros([DELAY_STEPS, nx, nV])
-    for v in range(nV):
-        Y = scipy.integrate.odeint(scenario.model.ode, x_measured[v, :], times,
-                                   args=(u_path[v, -1], scenario.Lf[v], scenario.Lr[v]))
-        x0[v, :] = Y[-1, :]
-        u0[v, :] = u_path[v, -1]
-        traj[:, :, v] = Y
-    return x0, u0, traj
+    from scpqp import plant
+    params = plant.plant_params(scenario.Lf, scenario.Lr)
+    x_meas = np.asarray(x_measured, float).reshape(1, nV, nx)
+    u_hold = np.asarray(u_path, float)[:, -1].reshape(1, nV)
+    x0d, trajd = plant.delay_compensate(params, x_meas, u_hold, horizon, n_out=DELAY_STEPS)
+    u0 = u_hold.reshape(nV, nu).copy()
+    return x0d[0].cpu().numpy(), u0, trajd[0].cpu().numpy()
 
 
 def predict_obstacles(scenario, obstacleState):

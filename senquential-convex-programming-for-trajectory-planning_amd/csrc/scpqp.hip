@@ -2188,6 +2188,9 @@ KArgs base_args(int32_t B, const scpqp_batch_in* in) {
 
 }  // namespace
 
+// error reporting for the other translation units of the library (plant.hip)
+int scpqp_fail_(int code, const char* msg) { return fail(code, "%s", msg); }
+
 extern "C" {
 
 const char* scpqp_last_error(void) { return g_err; }

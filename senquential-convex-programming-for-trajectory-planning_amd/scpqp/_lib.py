@@ -72,9 +72,15 @@ class EvalOut(C.Structure):
                 ("c_obs", C.c_void_p), ("traj", C.c_void_p)]
 
 
+class PlantParams(C.Structure):
+    _fields_ = [("n_veh", C.c_int32), ("pad0", C.c_int32), ("lf", C.c_double * MAX_VEH),
+                ("lr", C.c_double * MAX_VEH)]
+
+
 # every symbol include/scpqp.h declares (checked by tests/test_abi.py)
 EXPORTS = ("scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version", "scpqp_solve",
-           "scpqp_linearize", "scpqp_evaluate", "scpqp_sample_reference", "scpqp_resources")
+           "scpqp_linearize", "scpqp_evaluate", "scpqp_sample_reference", "scpqp_resources",
+           "scpqp_delay_compensate", "scpqp_plant_step", "scpqp_clip_controls")
 
 _lib = None
 
@@ -109,6 +115,16 @@ def load(path=None):
     lib.scpqp_resources.argtypes = [H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                     C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.scpqp_resources.restype = C.c_int
+    PP = C.POINTER(PlantParams)
+    V = C.c_void_p
+    lib.scpqp_delay_compensate.argtypes = [PP, C.c_int32, C.c_double, C.c_int32, V, V, V, V, V,
+                                           C.c_double, V]
+    lib.scpqp_delay_compensate.restype = C.c_int
+    lib.scpqp_plant_step.argtypes = [PP, C.c_int32, C.c_int32, C.c_double, V, V, V, V, C.c_double, V]
+    lib.scpqp_plant_step.restype = C.c_int
+    lib.scpqp_clip_controls.argtypes = [C.c_int32, C.c_int32, C.c_int32, C.c_int32, C.c_double,
+                                        V, V, V, V]
+    lib.scpqp_clip_controls.restype = C.c_int
     if path is None:
         _lib = lib
     return lib

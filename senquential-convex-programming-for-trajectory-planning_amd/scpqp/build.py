@@ -1,4 +1,4 @@
-"""Build the HIP library in-tree: csrc/scpqp.hip -> scpqp/libscpqp.so (gfx950)."""
+"""Build the HIP library in-tree: csrc/scpqp.hip + csrc/plant.hip -> scpqp/libscpqp.so (gfx950)."""
 from __future__ import annotations
 
 import os
@@ -9,6 +9,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)
 _REPO = os.path.dirname(_ROOT)
 SRC = os.path.join(_ROOT, "csrc", "scpqp.hip")
+SRCS = [SRC, os.path.join(_ROOT, "csrc", "plant.hip")]
 INCLUDE = os.path.join(_REPO, "include")
 LIB_PATH = os.path.join(_PKG, "libscpqp.so")
 ARCH = os.environ.get("SCPQP_ARCH", "gfx950")
@@ -20,14 +21,14 @@ def build_library(force=False, verbose=False, defines=(), out=None):
     ``defines``/``out`` build a diagnostic variant (e.g. ``("SCPQP_PROF",)`` ->
     ``libscpqp_prof.so``); the shipped library is built with neither."""
     out = out or LIB_PATH
-    deps = [SRC, os.path.join(INCLUDE, "scpqp.h"), __file__]
+    deps = SRCS + [os.path.join(INCLUDE, "scpqp.h"), __file__]
     if not force and os.path.exists(out):
         t = os.path.getmtime(out)
         if all(os.path.getmtime(d) <= t for d in deps):
             return out
     cmd = ["hipcc", f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", f"-I{INCLUDE}"] + [f"-D{d}" for d in defines] + \
-          [SRC, "-o", out + ".tmp"]
+          SRCS + ["-o", out + ".tmp"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)

@@ -1,0 +1,140 @@
+"""Closed-loop Monte-Carlo rollouts on the GPU (main.py:98-206).
+
+``ClosedLoopBatch`` runs ``Simulation.runsimulation`` with the SCP controller
+for B independent realisations of one scenario at once.  Per MPC step i:
+
+1. measurement, steering limits and the held command (main.py:101-117, 105-108)
+2. delay compensation, ``IterClass`` (MPC_Iter.py:24-33)   -> scpqp_delay_compensate
+3. the SCP solve, warm-started from the previous step's u  -> scpqp_solve
+   (SCP_controller.py:42-43)
+4. steering-limit enforcement (main.py:164-174)            -> scpqp_clip_controls
+5. actuator-delayed control path and the plant over one step (main.py:176-191)
+                                                            -> scpqp_plant_step
+
+All state lives on the device (torch-ROCm tensors); the per-step index
+bookkeeping (which tick is measured, which control tick each plant output
+reads) is the same for every realisation and is computed on the host once
+per step, exactly as main.py computes it.  Realisations differ by their
+initial state (and optional constant model-noise terms).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import plant as PL
+from .solver import ScpQpSolver
+
+LATERAL_ACC_LIMIT = 9.81 / 2      # Scenarios.py:48
+
+
+class ClosedLoopBatch:
+    def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, **solver_kw):
+        self.sc = scenario
+        self.B = int(B)
+        self.device = torch.device(device or "cuda")
+        self.nV, self.Hp = int(scenario.nVeh), int(scenario.Hp)
+        self.tps = int(scenario.ticks_per_sim)
+        self.ticks_total = int(scenario.ticks_total)
+        self.tdx, self.tdu = int(scenario.ticks_delay_x), int(scenario.ticks_delay_u)
+        if self.tdx > self.tps:
+            raise ValueError("measurement delay longer than one MPC step is not supported")
+        self.h_max = h_max
+        self.keep_path = keep_path
+        self.params = PL.plant_params(scenario.Lf, scenario.Lr)
+        self.solver = ScpQpSolver(scenario, max_batch=self.B, device=self.device, **solver_kw)
+        self.du_lim = float(scenario.mechanicalSteeringLimit) * 2          # Scenarios.py:50
+        f = dict(dtype=torch.float64, device=self.device)
+        self.L = torch.tensor([float(a) + float(b) for a, b in zip(scenario.Lf, scenario.Lr)], **f)
+        self.control = torch.full((self.B, self.nV, self.ticks_total + 1), float("nan"), **f)
+        self.state = torch.zeros((self.B, self.nV, 6), **f)
+        self.last_path = None          # [B, nV, tps + 1, 6] of the previous step
+        self.u_prev = None
+        self.out = self.solver.alloc_out(self.B)
+        self.history = []
+
+    def reset(self, x_init, noise=None):
+        """main.py:73-75: vehiclePathFullRes[:, v, 0] = x0; the control path holds
+        scenario.u0 for the first ticks_delay_u + ticks_per_sim + 1 ticks."""
+        x = torch.as_tensor(np.asarray(x_init, float) if not isinstance(x_init, torch.Tensor)
+                            else x_init, dtype=torch.float64, device=self.device)
+        if tuple(x.shape) != (self.B, self.nV, 6):
+            raise ValueError("x_init must be [B, nVeh, 6]")
+        self.state.copy_(x)
+        self.control.fill_(float("nan"))
+        u0 = torch.tensor([float(u) for u in self.sc.u0], dtype=torch.float64, device=self.device)
+        self.control[:, :, 0:self.tdu + self.tps + 1] = u0[None, :, None]
+        self.noise = None if noise is None else torch.as_tensor(noise, dtype=torch.float64,
+                                                                device=self.device)
+        self.last_path = None
+        self.u_prev = None
+        self.history = []
+        self.i = 0
+
+    def _held_command(self, tick_now):
+        """u_path[:, -1] of main.py:113-117: the control tick it copies, or None
+        when the slice is truncated at the end of the simulation (u_path stays 0)."""
+        tick_meas = max(0, tick_now - self.tdx)
+        tick_act = min(self.ticks_total + 1, tick_now + 1 + self.tdu + self.tps)
+        n_path = self.tdx + self.tps + self.tdu
+        lo = max(self.tdx - tick_now, 0)
+        hi = lo + tick_act - 1 - tick_meas
+        if hi < n_path:
+            return None
+        return tick_meas + 1 + (n_path - 1 - lo)
+
+    def step(self):
+        i, sc, B, nV, Hp, tps = self.i, self.sc, self.B, self.nV, self.Hp, self.tps
+        f = dict(dtype=torch.float64, device=self.device)
+        tick_now = i * tps
+        # measured state: tick_now - ticks_delay_x (inside the previous step's path)
+        if self.tdx == 0 or self.last_path is None:
+            x_meas = self.state
+        else:
+            x_meas = self.last_path[:, :, tps - min(self.tdx, tick_now), :].contiguous()
+        speed = self.state[:, :, 3]
+        umax = torch.minimum(torch.full_like(speed, float(sc.mechanicalSteeringLimit)),
+                             torch.atan(LATERAL_ACC_LIMIT * self.L[None, :] / speed ** 2))
+        src = self._held_command(tick_now)
+        u_hold = torch.zeros((B, nV), **f) if src is None else self.control[:, :, src].contiguous()
+        # IterClass delay compensation (MPC_Iter.py:24-33)
+        horizon = sc.delay_x + sc.dt + sc.delay_u
+        x0, dtraj = PL.delay_compensate(self.params, x_meas.contiguous(), u_hold, horizon,
+                                        noise=self.noise, h_max=self.h_max, device=self.device)
+        # SCP solve, warm-started from the previous controller output (SCP_controller.py:42-43)
+        out = self.solver.solve(x0, u_hold, u_warm=self.u_prev, out=self.out)
+        self.u_prev = out.u.clone()
+        U = out.u.clone()
+        PL.clip_controls(U, u_hold, umax, nV, Hp, self.du_lim)
+        # actuator-delayed control path (main.py:176-182)
+        sl = np.arange(i * tps + 1 + self.tdu + tps, (i + 1) * tps + 1 + self.tdu + tps)
+        sl[sl >= self.ticks_total] = self.ticks_total
+        sl_t = torch.as_tensor(np.unique(sl), device=self.device)
+        first = U.view(B, nV, -1)[:, :, 0]
+        self.control[:, :, sl_t] = first[:, :, None].expand(B, nV, len(sl_t))
+        # plant over [i dt, (i+1) dt]: output k reads control tick ceil(t_k / tick) + 1
+        timelist = np.linspace(i * sc.dt, (i + 1) * sc.dt, tps + 1)
+        idx = [min(self.ticks_total, math.ceil(t / sc.tick_length) + 1) for t in timelist]
+        u_tick = self.control[:, :, torch.as_tensor(idx, device=self.device)].contiguous()
+        path = PL.plant_step(self.params, self.state, u_tick, sc.tick_length, noise=self.noise,
+                             h_max=self.h_max, device=self.device)
+        self.last_path = path
+        self.state = path[:, :, tps, :].contiguous()
+        rec = dict(x0=x0, u0=u_hold, umax=umax, U=U, traj=out.traj.clone(),
+                   n_scp=out.n_scp.clone(), status=out.status.clone())
+        if self.keep_path:
+            rec["path"] = path
+            rec["delay_traj"] = dtraj
+        self.history.append(rec)
+        self.i += 1
+        return rec
+
+    def run(self, n_steps):
+        for _ in range(n_steps):
+            self.step()
+        return self.history
+
+    def close(self):
+        self.solver.close()

@@ -32,7 +32,8 @@ def test_header_declares_the_boundary():
     fns = header_functions()
     assert fns == sorted(["scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version",
                           "scpqp_solve", "scpqp_linearize", "scpqp_evaluate",
-                          "scpqp_sample_reference", "scpqp_resources"])
+                          "scpqp_sample_reference", "scpqp_resources",
+                          "scpqp_delay_compensate", "scpqp_plant_step", "scpqp_clip_controls"])
     assert sorted(LB.EXPORTS) == fns
 
 
@@ -68,6 +69,24 @@ def test_argument_validation_without_gpu(lib):
     bi = LB.BatchIn()
     bo = LB.BatchOut()
     assert lib.scpqp_solve(None, 1, C.byref(bi), C.byref(bo), None) == -1
+    # plant entry points: validation before any launch; B = 0 is a no-op
+    pp = LB.PlantParams(n_veh=0)
+    assert lib.scpqp_delay_compensate(C.byref(pp), 1, 0.43, 10, None, None, None, None, None,
+                                      2.5e-3, None) == -1
+    pp = LB.PlantParams(n_veh=2)
+    pp.lf[0] = pp.lr[0] = pp.lf[1] = pp.lr[1] = 0.34
+    assert lib.scpqp_delay_compensate(C.byref(pp), 1, 0.43, 1, None, None, None, None, None,
+                                      2.5e-3, None) == -1                  # n_out < 2
+    assert lib.scpqp_delay_compensate(C.byref(pp), 0, 0.43, 10, None, None, None, None, None,
+                                      2.5e-3, None) == 0
+    assert lib.scpqp_delay_compensate(C.byref(pp), 3, 0.43, 10, None, None, None, None, None,
+                                      2.5e-3, None) == -1                  # null arrays
+    assert lib.scpqp_plant_step(C.byref(pp), 1, 40, 0.0, None, None, None, None, 2.5e-3,
+                                None) == -1                                # tick <= 0
+    assert lib.scpqp_plant_step(C.byref(pp), 0, 40, 0.01, None, None, None, None, 2.5e-3,
+                                None) == 0
+    assert lib.scpqp_clip_controls(1, 2, 10, 19, 0.1, None, None, None, None) == -1   # ld < nV*hp
+    assert lib.scpqp_clip_controls(0, 2, 10, 20, 0.1, None, None, None, None) == 0
 
 
 PROBE = r"""
@@ -78,6 +97,7 @@ PROBE = r"""
 #define O(t, f) printf(#t "." #f " %zu\n", offsetof(t, f));
 int main(void) {
   S(scpqp_dims) S(scpqp_params) S(scpqp_batch_in) S(scpqp_batch_out) S(scpqp_lin_out) S(scpqp_eval_out)
+  S(scpqp_plant_params)
   %s
   return 0;
 }
@@ -87,7 +107,7 @@ int main(void) {
 def test_ctypes_layout_matches_header(tmp_path):
     structs = {"scpqp_dims": LB.Dims, "scpqp_params": LB.Params, "scpqp_batch_in": LB.BatchIn,
                "scpqp_batch_out": LB.BatchOut, "scpqp_lin_out": LB.LinOut,
-               "scpqp_eval_out": LB.EvalOut}
+               "scpqp_eval_out": LB.EvalOut, "scpqp_plant_params": LB.PlantParams}
     offs = "".join(f"O({cn}, {f}) " for cn, cls in structs.items() for f, _ in cls._fields_)
     src = tmp_path / "probe.c"
     src.write_text(PROBE.replace("%s", offs))

@@ -1,0 +1,163 @@
+"""GPU parity of the plant kernels (csrc/plant.hip) and the
+closed-loop rollout against the CPU restatement (oracle/plant_reference.py).
+
+Tolerances: the device integrates with fixed-step RK4 (h <= 2.5 ms); against
+the integration-error-free DOP853 solution at rtol = atol = 1e-13 the states
+agree to 1e-9; against the reference's own scipy calls (odeint at 1.49e-8,
+dopri5 at 1e-8) to 1e-6.  Clipping is min/max arithmetic: bit-exact.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import plant_reference as PR
+from oracle import scp_reference as R
+from scpqp import plant as PL
+
+pytestmark = pytest.mark.gpu
+
+
+def _states(rng, B, V):
+    x = np.zeros((B, V, 6))
+    x[..., 0] = rng.uniform(-30, 30, (B, V))
+    x[..., 1] = rng.uniform(-30, 30, (B, V))
+    x[..., 2] = rng.uniform(-math.pi, math.pi, (B, V))
+    x[..., 3] = rng.uniform(2.0, 6.0, (B, V))
+    x[..., 4] = rng.uniform(-0.5, 0.5, (B, V))
+    x[..., 5] = rng.uniform(-0.05, 0.05, (B, V))
+    return x
+
+
+def test_delay_compensate_parity(gpu):
+    sc = R.circle_scenario(4, Hp=20)
+    rng = np.random.default_rng(11)
+    B, V = 24, 4
+    xm = _states(rng, B, V)
+    uh = rng.uniform(-0.05, 0.05, (B, V))
+    p = PL.plant_params(sc.Lf, sc.Lr)
+    x0, traj = PL.delay_compensate(p, xm, uh, PR.delay_horizon(sc), device=gpu)
+    x0, traj = x0.cpu().numpy(), traj.cpu().numpy()
+    worst_exact = worst_ref = 0.0
+    for b in range(B):
+        xe, te = PR.delay_compensate_exact(sc, xm[b], uh[b])
+        xr, _, tr = PR.delay_compensate(sc, xm[b], uh[b])
+        worst_exact = max(worst_exact, np.abs(traj[b] - te).max(), np.abs(x0[b] - xe).max())
+        worst_ref = max(worst_ref, np.abs(traj[b] - tr).max())
+        assert np.array_equal(traj[b, -1].T, x0[b])
+    assert worst_exact < 1e-9, worst_exact
+    assert worst_ref < 1e-6, worst_ref
+
+
+def test_delay_compensate_noise_terms(gpu):
+    """Constant noise on dx[0], dx[1] shifts x, y by noise * T exactly (Model.py:84-86)."""
+    sc = R.circle_scenario(2, Hp=10)
+    p = PL.plant_params(sc.Lf, sc.Lr)
+    xm = np.array([[[0.0, 0.0, 0.3, 4.0, 0.0, 0.0], [1.0, 2.0, -0.3, 3.0, 0.0, 0.0]]])
+    nz = np.array([[[3e-6, -2e-6], [1e-6, 1e-6]]])
+    a, _ = PL.delay_compensate(p, xm, np.zeros((1, 2)), 0.43, device=gpu)
+    b, _ = PL.delay_compensate(p, xm, np.zeros((1, 2)), 0.43, noise=nz, device=gpu)
+    d = (b - a).cpu().numpy()[0]
+    assert np.allclose(d[:, :2], nz[0] * 0.43, atol=1e-15)
+    assert np.all(d[:, 2:] == 0)
+
+
+def test_plant_step_parity(gpu):
+    sc = R.circle_scenario(4, Hp=20)
+    rng = np.random.default_rng(5)
+    B, V, K = 6, 4, sc.ticks_per_sim + 1
+    xs = _states(rng, B, V)
+    ut = rng.uniform(-0.05, 0.05, (B, V, K))
+    p = PL.plant_params(sc.Lf, sc.Lr)
+    path = PL.plant_step(p, xs, ut, sc.tick_length, device=gpu).cpu().numpy()
+    assert path.shape == (B, V, K, 6)
+    worst_exact = worst_ref = 0.0
+    for b in range(2):
+        for v in range(V):
+            ex = PR.plant_step_exact(sc, v, xs[b, v], 1.2, ut[b, v])
+            rf = PR.plant_step(sc, v, xs[b, v], 1.2, ut[b, v])
+            worst_exact = max(worst_exact, np.abs(path[b, v] - ex).max())
+            worst_ref = max(worst_ref, np.abs(path[b, v] - rf).max())
+    assert np.array_equal(path[:, :, 0], xs)
+    assert worst_exact < 1e-9, worst_exact
+    assert worst_ref < 1e-6, worst_ref
+
+
+def test_clip_controls_bit_exact(gpu):
+    rng = np.random.default_rng(2)
+    B, V, Hp = 16, 4, 20
+    u = rng.uniform(-0.2, 0.2, (B, V * Hp))
+    u0 = rng.uniform(-0.05, 0.05, (B, V))
+    um = rng.uniform(0.02, 0.06, (B, V))
+    du = math.pi / 180 * 6
+    ut = torch.as_tensor(u, device=gpu).contiguous()
+    PL.clip_controls(ut, u0, um, V, Hp, du)
+    got = ut.cpu().numpy()
+    for b in range(B):
+        want = PR.clip_controls(u[b].reshape(V, Hp).T, u0[b], um[b], du).T.reshape(-1)
+        assert np.array_equal(got[b], want)
+
+
+def test_empty_batches(gpu):
+    p = PL.plant_params([0.34], [0.34])
+    x0, traj = PL.delay_compensate(p, np.zeros((0, 1, 6)), np.zeros((0, 1)), 0.43, device=gpu)
+    assert x0.shape == (0, 1, 6) and traj.shape == (0, 10, 6, 1)
+    out = PL.plant_step(p, np.zeros((0, 1, 6)), np.zeros((0, 1, 41)), 0.01, device=gpu)
+    assert out.shape == (0, 1, 41, 6)
+    with pytest.raises(ValueError):
+        PL.delay_compensate(p, np.zeros((2, 2, 6)), np.zeros((2, 2)), 0.43, device=gpu)
+
+
+def test_closed_loop_rollout_matches_restatement(gpu):
+    """Three MPC steps of main.py:98-191 for two realisations (perturbed initial
+    states): delay compensation, warm-started SCP, clipping, plant."""
+    from scpqp.rollout import ClosedLoopBatch
+    sc = R.circle_scenario(4, Hp=10)
+    rng = np.random.default_rng(7)
+    B, steps = 2, 3
+    base = np.array(sc.x0)
+    x_init = base[None] + rng.normal(0, 1, (B, 4, 6)) * np.array([0.05, 0.05, 0.005, 0.02, 0, 0.002])
+    cl = ClosedLoopBatch(sc, B, device=gpu, keep_path=True)
+    cl.reset(x_init)
+    hist = cl.run(steps)
+    for b in range(B):
+        ref = PR.ClosedLoop(sc, x_init=x_init[b])
+        for i in range(steps):
+            r = ref.step(i)
+            h = hist[i]
+            assert np.abs(h["x0"][b].cpu().numpy() - r["x0"]).max() < 1e-6
+            assert np.abs(h["umax"][b].cpu().numpy() - r["umax"]).max() < 1e-12
+            if int(h["n_scp"][b]) == r["n_scp"]:
+                U = h["U"][b].cpu().numpy().reshape(4, 10).T
+                assert np.abs(U - r["U"]).max() < 1e-6
+                path = h["path"][b].cpu().numpy()             # [V, K, 6]
+                tps = sc.ticks_per_sim
+                want = ref.path[:, :, i * tps:(i + 1) * tps + 1].transpose(1, 2, 0)
+                assert np.abs(path - want).max() < 1e-5
+    cl.close()
+
+
+def test_dropin_delay_compensation_matches_straight_line_and_odeint(gpu):
+    """MPC_Iter.delay_compensate (the drop-in IterClass path) runs on the device."""
+    import MPC_Iter
+    import Scenarios
+    from scpqp import batch as BT
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = 20
+    sc.get_circle_scenario([2 * math.pi / 4 * (i + 1) for i in range(4)])
+    sc.complete_scenario()
+    nT = sc.ticks_delay_x + sc.ticks_per_sim + sc.ticks_delay_u
+    x_meas = np.array(sc.x0).reshape(4, 6)
+    u_path = np.zeros((4, nT))
+    x0, u0, traj = MPC_Iter.delay_compensate(sc, x_meas, u_path)
+    assert np.allclose(x0, BT.delay_compensated_nominal(sc), atol=1e-10)
+    assert traj.shape == (10, 6, 4) and np.array_equal(traj[-1].T, x0)
+    assert np.all(u0 == 0)
+    u_path[:, -1] = [0.01, -0.02, 0.03, 0.0]
+    x0, u0, traj = MPC_Iter.delay_compensate(sc, x_meas, u_path)
+    osc = R.circle_scenario(4, Hp=20)
+    xr, _, tr = PR.delay_compensate(osc, x_meas, u_path[:, -1])
+    assert np.abs(traj - tr).max() < 1e-6 and np.allclose(u0[:, 0], u_path[:, -1])
+    with pytest.raises(AssertionError):
+        MPC_Iter.delay_compensate(sc, x_meas, np.zeros((4, nT + 1)))

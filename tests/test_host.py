@@ -110,20 +110,6 @@ def test_sampler_argument_check_raises_before_launch():
         SampleReferTraj.sampleReferenceTrajectory(5, np.array([[0, 0], [1, 0]]), 0.0, 0.0, 1.6)
 
 
-def test_delay_compensation_matches_straight_line_and_odeint():
-    sc = _circle(4, hp=20)
-    nT = sc.ticks_delay_x + sc.ticks_per_sim + sc.ticks_delay_u
-    x_meas = np.array(sc.x0).reshape(4, 6)
-    u_path = np.zeros((4, nT))
-    x0, u0, traj = MPC_Iter.delay_compensate(sc, x_meas, u_path)
-    nominal = BT.delay_compensated_nominal(sc)
-    assert np.allclose(x0, nominal, atol=1e-6)
-    assert traj.shape == (10, 6, 4) and np.array_equal(traj[-1].T, x0)
-    assert np.all(u0 == 0)
-    with pytest.raises(AssertionError):
-        MPC_Iter.delay_compensate(sc, x_meas, np.zeros((4, nT + 1)))
-
-
 def test_obstacle_prediction_matches_restatement():
     sc = Scenarios.Scenario(False)
     sc.Hp = sc.Hu = 12
