@@ -139,6 +139,35 @@ def control_tick_index(sc, t):
     return min(sc.ticks_total, math.ceil(t / sc.tick_length) + 1)
 
 
+def evaluate_in_original_problem(sc, U, traj, ref_points, obst_future=None,
+                                 tol=R.CONSTRAINT_TOL):
+    """SCP_controller.py:343-400 (evaluateInOriginalProblem) without the QCQP
+    re-check: U [Hp, nVeh] (controller output), traj [Hp, 2, nVeh], ref_points
+    [Hp, 2, nVeh], obst_future [nObst, 2, Hp]."""
+    nV, Hp = U.shape[1], U.shape[0]
+    err2 = (ref_points - traj) ** 2
+    objx = sum(sc.Q[v] * err2[:-1, :, v].sum() + sc.Q_final[v] * err2[-1, :, v].sum()
+               for v in range(nV))
+    obju = sum(sc.R[v] * (U[:, v] ** 2).sum() for v in range(nV))
+    cv = np.zeros((nV, nV, Hp))
+    nO = 0 if obst_future is None else obst_future.shape[0]
+    co = np.zeros((nV, nO, Hp))
+    feasible = True
+    for k in range(Hp):
+        for v in range(nV):
+            for v2 in range(v + 1, nV):
+                ci = sc.dsafeVehicles[v, v2] ** 2 - ((traj[k, :, v] - traj[k, :, v2]) ** 2).sum()
+                cv[v, v2, k] = cv[v2, v, k] = ci
+                feasible = feasible and not ci > tol
+            for o in range(nO):
+                ci = sc.dsafeObstacles[v, o] ** 2 - ((traj[k, :, v] - obst_future[o, :, k]) ** 2).sum()
+                co[v, o, k] = ci
+                feasible = feasible and not ci > tol
+    return dict(predictionObjectiveValueX=objx, predictionObjectiveValueU=obju,
+                predictionObjectiveValue=objx + obju, constraintValuesVehicle=cv,
+                constraintValuesObstacle=co, predictionFeasible=feasible)
+
+
 class ClosedLoop:
     """Restatement of ``Simulation.runsimulation`` (main.py:98-206) for one
     realisation with the SCP controller of ``scp_reference`` (structured mode).
@@ -182,6 +211,7 @@ class ClosedLoop:
             u_of_k = [self.control[v, control_tick_index(sc, t)] for t in timelist]
             ms = plant_step(sc, v, self.path[:, v, tick_now], i * sc.dt, u_of_k)
             self.path[:, v, tps * i + 1:tps * (i + 1) + 1] = ms[1:].T
+        ev = evaluate_in_original_problem(sc, U, res.traj, p.ref_points)
         self.records.append(dict(x0=x0, u0=u0, delay_traj=dtraj, umax=umax, U=U, traj=res.traj,
-                                 n_scp=res.n_scp, u=res.u))
+                                 n_scp=res.n_scp, u=res.u, evaluation=ev))
         return self.records[-1]

@@ -10,6 +10,8 @@ for B independent realisations of one scenario at once.  Per MPC step i:
 4. steering-limit enforcement (main.py:164-174)            -> scpqp_clip_controls
 5. actuator-delayed control path and the plant over one step (main.py:176-191)
                                                             -> scpqp_plant_step
+6. evaluateInOriginalProblem of the step (main.py:201-202, SCP_controller.py:343-400)
+                                                            -> device tensor ops
 
 All state lives on the device (torch-ROCm tensors); the per-step index
 bookkeeping (which tick is measured, which control tick each plant output
@@ -28,10 +30,48 @@ from . import plant as PL
 from .solver import ScpQpSolver
 
 LATERAL_ACC_LIMIT = 9.81 / 2      # Scenarios.py:48
+CONSTRAINT_TOL = 2 * 2.1 * 1e-3   # Config.py:18
+
+
+def evaluate_in_original_problem(scenario, U, traj, ref_points, obst_future=None,
+                                 tol=CONSTRAINT_TOL):
+    """SCPcontroller.evaluateInOriginalProblem (SCP_controller.py:343-400) for a
+    batch, on the device: U [B, Hp, nVeh] (the clipped controller output),
+    traj [B, Hp, 2, nVeh] (trajectory prediction), ref_points [B, Hp, 2, nVeh],
+    obst_future [B, nObst, 2, Hp] or None.  Returns tensors: the objective terms
+    [B], constraint values [B, nVeh, nVeh, Hp] / [B, nVeh, nObst, Hp] and
+    predictionFeasible [B] (from the predicted trajectory, as the reference)."""
+    dev = U.device
+    f = dict(dtype=torch.float64, device=dev)
+    nV = U.shape[2]
+    Q = torch.tensor([float(q) for q in scenario.Q], **f)
+    Qf = torch.tensor([float(q) for q in scenario.Q_final], **f)
+    Rw = torch.tensor([float(r) for r in scenario.R], **f)
+    err2 = (ref_points - traj) ** 2                                  # [B, Hp, 2, nV]
+    objx = (err2[:, :-1].sum(dim=(1, 2)) * Q).sum(-1) + (err2[:, -1].sum(dim=1) * Qf).sum(-1)
+    obju = ((U ** 2).sum(dim=1) * Rw).sum(-1)
+    ds2 = torch.as_tensor(np.asarray(scenario.dsafeVehicles, float) ** 2, **f)   # [nV, nV]
+    p = traj.permute(0, 3, 2, 1)                                     # [B, nV, 2, Hp]
+    d2 = ((p[:, :, None] - p[:, None, :]) ** 2).sum(3)               # [B, nV, nV, Hp]
+    cv = ds2[None, :, :, None] - d2
+    eye = torch.eye(nV, dtype=torch.bool, device=dev)[None, :, :, None]
+    cv = torch.where(eye, torch.zeros_like(cv), cv)                  # diagonal stays 0
+    viol = (cv > tol).flatten(1).any(1)
+    out = dict(predictionObjectiveValueX=objx, predictionObjectiveValueU=obju,
+               predictionObjectiveValue=objx + obju, constraintValuesVehicle=cv)
+    if obst_future is not None and obst_future.shape[1] > 0:
+        dso = torch.as_tensor(np.asarray(scenario.dsafeObstacles, float) ** 2, **f)  # [nV, nO]
+        d2o = ((p[:, :, None] - obst_future[:, None]) ** 2).sum(3)   # [B, nV, nO, Hp]
+        co = dso[None, :, :, None] - d2o
+        viol = viol | (co > tol).flatten(1).any(1)
+        out["constraintValuesObstacle"] = co
+    out["predictionFeasible"] = ~viol
+    return out
 
 
 class ClosedLoopBatch:
-    def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, **solver_kw):
+    def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, evaluate=True,
+                 **solver_kw):
         self.sc = scenario
         self.B = int(B)
         self.device = torch.device(device or "cuda")
@@ -43,6 +83,9 @@ class ClosedLoopBatch:
             raise ValueError("measurement delay longer than one MPC step is not supported")
         self.h_max = h_max
         self.keep_path = keep_path
+        self.evaluate = evaluate
+        if scenario.nObst:
+            raise ValueError("obstacle scenarios: the batched rollout covers nObst = 0")
         self.params = PL.plant_params(scenario.Lf, scenario.Lr)
         self.solver = ScpQpSolver(scenario, max_batch=self.B, device=self.device, **solver_kw)
         self.du_lim = float(scenario.mechanicalSteeringLimit) * 2          # Scenarios.py:50
@@ -124,6 +167,11 @@ class ClosedLoopBatch:
         self.state = path[:, :, tps, :].contiguous()
         rec = dict(x0=x0, u0=u_hold, umax=umax, U=U, traj=out.traj.clone(),
                    n_scp=out.n_scp.clone(), status=out.status.clone())
+        if self.evaluate:
+            # main.py:201-202: evaluateInOriginalProblem on the clipped U and the prediction
+            ref = self.solver.sample_reference(x0)
+            rec["evaluation"] = evaluate_in_original_problem(
+                sc, U.view(B, nV, Hp).transpose(1, 2), rec["traj"], ref)
         if self.keep_path:
             rec["path"] = path
             rec["delay_traj"] = dtraj

@@ -135,6 +135,12 @@ def test_closed_loop_rollout_matches_restatement(gpu):
                 tps = sc.ticks_per_sim
                 want = ref.path[:, :, i * tps:(i + 1) * tps + 1].transpose(1, 2, 0)
                 assert np.abs(path - want).max() < 1e-5
+                ev, rev = h["evaluation"], r["evaluation"]     # SCP_controller.py:343-400
+                for k in ("predictionObjectiveValueX", "predictionObjectiveValueU"):
+                    assert abs(float(ev[k][b]) - rev[k]) <= 1e-6 * max(1.0, abs(rev[k]))
+                assert np.abs(ev["constraintValuesVehicle"][b].cpu().numpy()
+                              - rev["constraintValuesVehicle"]).max() < 1e-6
+                assert bool(ev["predictionFeasible"][b]) == rev["predictionFeasible"]
     cl.close()
 
 

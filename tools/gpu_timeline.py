@@ -49,3 +49,13 @@ order = np.argsort(-t[:, 1])[:12]
 print("last to finish: idx start end latency nscp nipm")
 for i in order:
     print(f"  {i:5d} {t[i, 0] / 1e3:6.2f} {t[i, 1] / 1e3:6.2f} {lat[i] / 1e3:6.2f} {nscp[i]:3d} {nipm[i]:4d}")
+
+# does a cheap pre-pass predict the cost?  QCQP_evaluate at u = 0 (the kernel's own first step)
+ev = S.evaluate(np.zeros((B, 4 * 20)), bt.x0, bt.u0, bt.ec_noise)
+feat = {"maxviol(u=0)": ev["max_violation"].cpu().numpy(), "sumviol(u=0)": ev["sum_violations"].cpu().numpy(),
+        "obj(u=0)": ev["obj"].cpu().numpy()}
+def spearman(a, b):
+    ra = np.argsort(np.argsort(a)); rb = np.argsort(np.argsort(b))
+    return float(np.corrcoef(ra, rb)[0, 1])
+for k, f in feat.items():
+    print(f"spearman({k}, latency) = {spearman(f, lat):+.3f}   (nipm) {spearman(f, nipm):+.3f}   (nscp) {spearman(f, nscp):+.3f}")
