@@ -188,13 +188,16 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
+    # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
+    # workload (tools/gpu_round.sh + tools/pmc_summary.py); measured on c2 only
     traffic = None
-    if os.path.exists(PMC_SUMMARY):
+    if args.config == "c2" and B == 1024 and os.path.exists(PMC_SUMMARY):
         try:
             with open(PMC_SUMMARY) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    res = S.resources()
 
     line = {
         "metric": METRIC,
@@ -217,6 +220,10 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "scp_kernel", "kernel_ms": kern_ms,
+                     "traffic_source": "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE)"
+                     if traffic is not None else None,
+                     "memory_plan": res["plan"], "lds_bytes": res["lds_bytes"],
+                     "workgroups": res["grid"],
                      "flops_per_launch": flops,
                      "peak_note": "FP64 dense peak (vector = MFMA rate on gfx950, AMD spec)"},
         "qp_solves_per_s": world * float(n_scp.sum()) * args.steps / elapsed,
