@@ -69,6 +69,21 @@ def evaluate_in_original_problem(scenario, U, traj, ref_points, obst_future=None
     return out
 
 
+def held_command_tick(tick_now, tdx, tdu, tps, ticks_total):
+    """u_path[:, -1] of main.py:101-117 (the command IterClass holds over the
+    delay, MPC_Iter.py:29-32): the controlPathFullRes tick it copies, or None
+    when the slice is truncated at the end of the simulation and u_path[:, -1]
+    keeps its zero initialisation."""
+    tick_meas = max(0, tick_now - tdx)
+    tick_act = min(ticks_total + 1, tick_now + 1 + tdu + tps)
+    n_path = tdx + tps + tdu
+    lo = max(tdx - tick_now, 0)
+    hi = lo + tick_act - 1 - tick_meas
+    if hi < n_path:
+        return None
+    return tick_meas + 1 + (n_path - 1 - lo)
+
+
 class ClosedLoopBatch:
     def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, evaluate=True,
                  **solver_kw):
@@ -117,16 +132,7 @@ class ClosedLoopBatch:
         self.i = 0
 
     def _held_command(self, tick_now):
-        """u_path[:, -1] of main.py:113-117: the control tick it copies, or None
-        when the slice is truncated at the end of the simulation (u_path stays 0)."""
-        tick_meas = max(0, tick_now - self.tdx)
-        tick_act = min(self.ticks_total + 1, tick_now + 1 + self.tdu + self.tps)
-        n_path = self.tdx + self.tps + self.tdu
-        lo = max(self.tdx - tick_now, 0)
-        hi = lo + tick_act - 1 - tick_meas
-        if hi < n_path:
-            return None
-        return tick_meas + 1 + (n_path - 1 - lo)
+        return held_command_tick(tick_now, self.tdx, self.tdu, self.tps, self.ticks_total)
 
     def step(self):
         i, sc, B, nV, Hp, tps = self.i, self.sc, self.B, self.nV, self.Hp, self.tps

@@ -128,3 +128,28 @@ def test_closed_loop_restatement_two_steps():
     # the command applied after the actuator delay is the first clipped control
     assert np.allclose(cl.control[:, 1 + sc.ticks_delay_u + tps], r0["U"][0])
     assert np.all(np.abs(r1["U"]) <= sc.mechanicalSteeringLimit + 1e-12)
+
+
+@pytest.mark.parametrize("tdx", [0, 2])
+def test_held_command_tick_matches_main_py_slicing(tdx):
+    """The rollout's held-command index (scpqp/rollout.py) against main.py:101-117's
+    u_path construction, over a whole simulation including the truncated end."""
+    from scpqp.rollout import held_command_tick
+    sc = _sc()
+    tps, tdu, tt = sc.ticks_per_sim, sc.ticks_delay_u, sc.ticks_total
+    control = np.arange(tt + 1, dtype=float) + 1.0          # tick k holds k + 1
+    truncated = 0
+    for i in range(sc.Nsim):
+        now = i * tps
+        meas = max(0, now - tdx)
+        act = min(tt + 1, now + 1 + tdu + tps)
+        u_path = np.zeros(tdx + tps + tdu)
+        lo = max(tdx - now, 0)
+        u_path[lo:lo + act - 1 - meas] = control[meas + 1:act]
+        k = held_command_tick(now, tdx, tdu, tps, tt)
+        if k is None:
+            truncated += 1
+            assert u_path[-1] == 0.0
+        else:
+            assert u_path[-1] == control[k]
+    assert truncated >= 1            # the last MPC step of main.py holds u = 0
