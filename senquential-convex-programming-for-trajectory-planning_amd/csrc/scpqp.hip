@@ -932,6 +932,7 @@ template <int RS, class HP>
 __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
                                              const ldouble* dprev, ldouble* dout, lint* flag) {
     const int lane = threadIdx.x & 63;
+    PROF_T0();
     double p[RS][CB];
     int ro[RS];
 #pragma unroll
@@ -945,31 +946,30 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
             p[t][c + 1] = v.y;
         }
     }
+#ifdef SCPQP_PROF
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    PROF_ACC(18);
     if (jp >= 0) {
-        // look-ahead update: p_ic -= sum_c' (L_ic' D_c') L_{r0+c, c'}
-        double li[RS][CB];
+        // look-ahead update p_ic -= sum_c' L_ic' (D_c' L_{r0+c, c'}).  Row r0 + c of
+        // the previous panel is lane c's own row (slot 0), so its D-scaled entries
+        // are broadcast with v_readlane instead of a serialised LDS broadcast load
+        double li[RS][CB], ld[CB];
 #pragma unroll
         for (int t = 0; t < RS; ++t)
 #pragma unroll
             for (int c = 0; c < CB; c += 2) {
                 const double2v v = ld2(H + ro[t] + jp + c);
-                li[t][c] = v.x * dprev[c];
-                li[t][c + 1] = v.y * dprev[c + 1];
+                li[t][c] = v.x;
+                li[t][c + 1] = v.y;
             }
+#pragma unroll
+        for (int c = 0; c < CB; ++c) ld[c] = li[0][c] * dprev[c];
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
-            // one broadcast row in flight at a time (keeps the panel within the
-            // register budget of 3 workgroups per CU)
-            asm volatile("" ::: "memory");
-            const int kr = r0 + c < n ? r0 + c : n - 1;
-            const int ko = roff(kr) + jp;
             double lk[CB];
 #pragma unroll
-            for (int c2 = 0; c2 < CB; c2 += 2) {
-                const double2v v = ld2(H + ko + c2);
-                lk[c2] = v.x;
-                lk[c2 + 1] = v.y;
-            }
+            for (int c2 = 0; c2 < CB; ++c2) lk[c2] = readlane_d(ld[c2], c);
 #pragma unroll
             for (int t = 0; t < RS; ++t) {
                 double sacc = 0.0;
@@ -986,6 +986,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         for (int c = 0; c < CB; ++c)
             p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
     }
+    PROF_ACC(19);
     int bad = 0;
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
@@ -1005,6 +1006,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
             dout[c] = D;
         }
     }
+    PROF_ACC(20);
 #pragma unroll
     for (int t = 0; t < RS; ++t) {
         const int i = r0 + lane + 64 * t;
@@ -1015,6 +1017,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         }
     }
     if (lane == 0) flag[0] = bad;
+    PROF_ACC(21);
 }
 
 // Rank-CB update of panel j0 (pivots dcur) on rows/columns >= r1, by threads
@@ -1088,7 +1091,14 @@ __device__ bool cholesky(const LT& L) {
         } else if (jp >= 0 && r1 < n) {
             trailing_update(L.H, n, jp, r1, dprev, (int)threadIdx.x - 64, NT - 64);
         }
+#ifdef SCPQP_PROF
+        unsigned long long _pb = __builtin_amdgcn_s_memtime();
+#endif
         __syncthreads();
+#ifdef SCPQP_PROF
+        if (threadIdx.x == 0) atomicAdd(&g_prof[22], __builtin_amdgcn_s_memtime() - _pb);
+        if (threadIdx.x == 64) atomicAdd(&g_prof[23], __builtin_amdgcn_s_memtime() - _pb);
+#endif
         if (flag[par]) return false;
     }
     PROF_ACC(13);

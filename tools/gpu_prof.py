@@ -15,7 +15,8 @@ from scpqp.solver import ScpQpSolver
 names = ["ipm-loop-top", "residuals", "assemble", "cholesky", "newton(pred)", "maxstep+corr",
          "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
          "chol:panel0", "chol:steps", "solve:fwd", "solve:bwd",   # 12-15: sub-phases of 3 / 9
-         "ipm-init", "take_u+evaluate"]
+         "ipm-init", "take_u+evaluate",
+         "panel:load", "panel:lookahead", "panel:pivots", "panel:store", "barrier-wait(w0)", "barrier-wait(w1)"]
 for nv, hp, B in [(4, 20, 1), (4, 20, 1024), (8, 30, 1)]:
     sc = R.circle_scenario(nv, Hp=hp)
     bt = BT.make_batch(sc, B, base_seed=1000)

@@ -19,13 +19,15 @@ from oracle import scp_reference as R  # noqa: E402
 from scpqp import batch as BT  # noqa: E402
 
 
-def polish(P, q, G, h, act, y_all, x, delta, rho=1e-12, nref=40, rounds=6, tol=1e-10, early=0.0, why=None):
+def polish(P, q, G, h, act, y_all, x, delta, rho=1e-12, nref=40, rounds=6, tol=1e-10, early=0.0, why=None,
+           stall=False):
     """Mirror of qp_polish_regularised from an explicit active set; returns
     (x, lam, n_solves, n_rounds) or (None, ..)."""
     xk = x.copy()
     L = None
     solves = 0
     extended = False
+    prev_chg = 1 << 30
     for rnd in range(rounds):
         Ga, ha = G[act], h[act]
         y = y_all[act].copy()
@@ -58,6 +60,11 @@ def polish(P, q, G, h, act, y_all, x, delta, rho=1e-12, nref=40, rounds=6, tol=1
             extended = True
             continue
         y_all[~nxt] = 0.0
+        nchg = int((nxt != act).sum())
+        if stall and rnd >= 1 and nchg >= prev_chg:
+            if why is not None: why.append('stall')
+            return None, None, solves, rnd + 1
+        prev_chg = nchg
         act = nxt
         L = None
     if why is not None: why.append('rounds')
@@ -69,11 +76,20 @@ def main():
     deltas = [3e-7]
     global NREF, ROUNDS, EARLY, WHY
     NREF, ROUNDS, EARLY = int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4])
+    global STALL; STALL = os.environ.get("STALL") == "1"
     WHY = []
     global TRACE; TRACE = []
+    global WROUNDS; WROUNDS = []
     global COARSE, CTOLS; COARSE = {}; CTOLS = [1e-3, 1e-4, 1e-5, 1e-6, 1e-7]
     sc = R.circle_scenario(4, Hp=20)
     bt = BT.make_batch(sc, nprob, base_seed=1234)
+    pick = os.environ.get("PROBLEMS")      # e.g. "1008,958": problems of the c2 bench batch
+    if pick:
+        idx = np.array([int(i) for i in pick.split(",")])
+        bt = BT.make_batch(sc, int(idx.max()) + 1, base_seed=0).slice(0, int(idx.max()) + 1)
+        bt = type(bt)(bt.x0[idx], bt.u0[idx], bt.ec_noise[idx], bt.hp[idx], bt.obst[idx], bt.hp_max,
+                      bt.seeds[idx])
+        nprob = len(idx)
     for delta in deltas:
         cold_s, warm_s, warm_ok, nqp, cold_r, warm_r, err = [], [], 0, 0, [], [], 0.0
         for b in range(nprob):
@@ -103,8 +119,9 @@ def main():
                     err = max(err, np.abs(xc * sv - hh["z"]).max())
                 if prev is not None:
                     pact, plam, px = prev
-                    xw, lw, nsw, nrw = polish(Ps, qs, Gs, hs, pact, plam, px, delta, nref=NREF, rounds=ROUNDS, early=EARLY, why=WHY)
+                    xw, lw, nsw, nrw = polish(Ps, qs, Gs, hs, pact, plam, px, delta, nref=NREF, rounds=ROUNDS, early=EARLY, why=WHY, stall=STALL)
                     warm_s.append(nsw); warm_r.append(nrw)
+                    WROUNDS.append((nrw, xw is not None))
                     warm_ok += xw is not None
                     TRACE.append((b, ih, len(r.history), xw is not None, nsw, int(pact.sum()), int((lc > 0).sum()) if xc is not None else -1, int((pact != (lc > 0)).sum()) if xc is not None else -1))
                 prev = (lc > 0, lc, xc) if xc is not None else None
@@ -116,6 +133,8 @@ def main():
         for ct, v in COARSE.items():
             v = np.array(v, float)
             print(f'   ipm tol {ct:.0e}: ipm its {v[:,1].mean():.2f} (full {v[:,0].mean():.2f}) polish ok {int(v[:,2].sum())}/{len(v)} solves {v[:,3].mean():.2f} rounds {v[:,4].mean():.2f} max rounds {v[:,4].max():.0f}')
+        wr = np.array(WROUNDS, float)
+        print(f"   warm rounds total {wr[:, 0].sum():.0f}  (successful attempts {wr[wr[:, 1] == 1, 0].sum():.0f}, failed {wr[wr[:, 1] == 0, 0].sum():.0f})")
         import collections
         agg = collections.defaultdict(lambda: [0, 0, 0])
         for t in TRACE:
