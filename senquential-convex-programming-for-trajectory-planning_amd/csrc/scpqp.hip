@@ -295,6 +295,40 @@ __device__ __forceinline__ void tri_decode(int t, int& i, int& k) {
     k = t - q * (q + 1) / 2;
 }
 
+// Tile t -> (vehicle block a >= b, tile row lt, tile column mt) of the K_uu
+// assembly, in order of increasing d = max(lt, mt): per d the V diagonal
+// blocks' d + 1 tiles (lt = d, mt <= d), then the PV off-diagonal blocks'
+// 2d + 1 tiles (lt = d, mt <= d; then mt = d, lt < d).
+__device__ __forceinline__ void tile_decode(int t, int V, int PV, int& a, int& b, int& lt, int& mt) {
+    int d = 0, base = 0;
+    for (;;) {
+        const int cnt = V * (d + 1) + PV * (2 * d + 1);
+        if (t < base + cnt) break;
+        base += cnt;
+        ++d;
+    }
+    int r = t - base;
+    if (r < V * (d + 1)) {
+        a = b = r / (d + 1);
+        lt = d;
+        mt = r - a * (d + 1);
+        return;
+    }
+    r -= V * (d + 1);
+    const int pr = r / (2 * d + 1), q = r - pr * (2 * d + 1);
+    int i_, k_;
+    tri_decode(pr, i_, k_);
+    a = i_ + 1;
+    b = k_;
+    if (q <= d) {
+        lt = d;
+        mt = q;
+    } else {
+        lt = q - (d + 1);
+        mt = d;
+    }
+}
+
 __device__ __forceinline__ int pair_index(int i, int j, int V) {
     return i * (2 * V - i - 1) / 2 + (j - i - 1);
 }
@@ -829,23 +863,19 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
     // columns m0, m0+1 of vehicle b, a >= b): per k one W~ block and four g
     // blocks serve four entries.  g indices below 0 read as zero, which gives
     // each entry its own lower summation bound max(l, l').
+    // A tile's cost is its trip count Hb - 2 max(lt, mt): tiles are enumerated by
+    // decreasing cost and dealt to the threads in snake order, so every thread
+    // gets about the same number of trips (c2: at most 32 against 54 for the
+    // block-by-block enumeration).
     const int N = L.N;
     const int TH = (Hb + 1) >> 1, TD = TH * (TH + 1) / 2, TO = TH * TH;
-    const int ntile = V * TD + (V * (V - 1) / 2) * TO;
-    for (int t = tid; t < ntile; t += NT) {
+    const int PV = V * (V - 1) / 2;
+    const int ntile = V * TD + PV * TO;
+    for (int r0 = 0; r0 < ntile; r0 += NT) {
+        const int t = r0 + (((r0 / NT) & 1) ? NT - 1 - tid : tid);
+        if (t >= ntile) continue;
         int a_, b_, lt, mt;
-        if (t < V * TD) {
-            a_ = b_ = t / TD;
-            tri_decode(t - a_ * TD, lt, mt);
-        } else {
-            const int t2 = t - V * TD, pr = t2 / TO, rem = t2 - pr * TO;
-            int i_, k_;
-            tri_decode(pr, i_, k_);
-            a_ = i_ + 1;
-            b_ = k_;
-            lt = rem / TH;
-            mt = rem - lt * TH;
-        }
+        tile_decode(t, V, PV, a_, b_, lt, mt);
         const int l0 = 2 * lt, m0 = 2 * mt;
         const ldouble* ga = L.g + a_ * Hb * 2;
         const ldouble* gb = L.g + b_ * Hb * 2;
