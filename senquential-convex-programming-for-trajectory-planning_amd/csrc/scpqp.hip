@@ -71,6 +71,15 @@ __device__ unsigned long long g_ptime[8192 * 2];   // per-problem [start, end] (
 #define PROF_T0() (void)0
 #define PROF_ACC(cat) (void)0
 #endif
+// Fine-grained stamps inside the factorisation (panel sub-phases, barrier waits):
+// only with -DSCPQP_PROF_FINE, since their atomics perturb whole-batch timelines.
+#if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
+#define PROF_T0_FINE() PROF_T0()
+#define PROF_ACC_FINE(cat) PROF_ACC(cat)
+#else
+#define PROF_T0_FINE() (void)0
+#define PROF_ACC_FINE(cat) (void)0
+#endif
 
 typedef __attribute__((address_space(3))) double ldouble;
 typedef __attribute__((address_space(3))) int lint;
@@ -962,7 +971,7 @@ template <int RS, class HP>
 __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
                                              const ldouble* dprev, ldouble* dout, lint* flag) {
     const int lane = threadIdx.x & 63;
-    PROF_T0();
+    PROF_T0_FINE();
     double p[RS][CB];
     int ro[RS];
 #pragma unroll
@@ -976,10 +985,10 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
             p[t][c + 1] = v.y;
         }
     }
-#ifdef SCPQP_PROF
+#ifdef SCPQP_PROF_FINE
     __builtin_amdgcn_s_waitcnt(0);
 #endif
-    PROF_ACC(18);
+    PROF_ACC_FINE(18);
     if (jp >= 0) {
         // look-ahead update p_ic -= sum_c' L_ic' (D_c' L_{r0+c, c'}).  Row r0 + c of
         // the previous panel is lane c's own row (slot 0), so its D-scaled entries
@@ -1016,7 +1025,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         for (int c = 0; c < CB; ++c)
             p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
     }
-    PROF_ACC(19);
+    PROF_ACC_FINE(19);
     int bad = 0;
 #pragma unroll
     for (int c = 0; c < CB; ++c) {
@@ -1036,7 +1045,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
             dout[c] = D;
         }
     }
-    PROF_ACC(20);
+    PROF_ACC_FINE(20);
 #pragma unroll
     for (int t = 0; t < RS; ++t) {
         const int i = r0 + lane + 64 * t;
@@ -1047,7 +1056,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         }
     }
     if (lane == 0) flag[0] = bad;
-    PROF_ACC(21);
+    PROF_ACC_FINE(21);
 }
 
 // Rank-CB update of panel j0 (pivots dcur) on rows/columns >= r1, by threads
@@ -1121,11 +1130,11 @@ __device__ bool cholesky(const LT& L) {
         } else if (jp >= 0 && r1 < n) {
             trailing_update(L.H, n, jp, r1, dprev, (int)threadIdx.x - 64, NT - 64);
         }
-#ifdef SCPQP_PROF
+#if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
         unsigned long long _pb = __builtin_amdgcn_s_memtime();
 #endif
         __syncthreads();
-#ifdef SCPQP_PROF
+#if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
         if (threadIdx.x == 0) atomicAdd(&g_prof[22], __builtin_amdgcn_s_memtime() - _pb);
         if (threadIdx.x == 64) atomicAdd(&g_prof[23], __builtin_amdgcn_s_memtime() - _pb);
 #endif

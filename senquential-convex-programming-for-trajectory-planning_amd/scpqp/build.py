@@ -38,7 +38,9 @@ def build_library(force=False, verbose=False, defines=(), out=None):
 
 if __name__ == "__main__":
     if "--prof" in sys.argv:
-        print(build_library(force="--force" in sys.argv, verbose=True, defines=("SCPQP_PROF",),
+        # --fine adds the factorisation sub-phase stamps (perturbs whole-batch timelines)
+        defs = ("SCPQP_PROF", "SCPQP_PROF_FINE") if "--fine" in sys.argv else ("SCPQP_PROF",)
+        print(build_library(force="--force" in sys.argv, verbose=True, defines=defs,
                             out=os.path.join(_PKG, "libscpqp_prof.so")))
     else:
         print(build_library(force="--force" in sys.argv, verbose=True))
