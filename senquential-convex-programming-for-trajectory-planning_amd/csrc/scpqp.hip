@@ -722,33 +722,63 @@ __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int 
 // ---------------------------------------------------------------------------
 // Structured linear operators (y-space = predicted-position space, [V][Hb][2])
 // ---------------------------------------------------------------------------
-// y[v][k] = sum_{l<=k} g[v][k-l] * x[v*Hb + l]     (calB x, MPC_Iter.py:146-147)
-template <class LT, class PX, class PY>
-__device__ __forceinline__ void toeplitz_apply(const LT& L, PX x, PY y) {
-    for (int e = threadIdx.x; e < L.V * L.Hb; e += NT) {
-        const int v = e / L.Hb, k = e % L.Hb;
-        const ldouble* gv = L.g + v * L.Hb * 2;
-        const int xb = v * L.Hb;
-        double a0 = 0.0, a1 = 0.0;
-        for (int l = 0; l <= k; ++l) {
-            const double xl = x[xb + l];
-            a0 += gv[(k - l) * 2] * xl;
-            a1 += gv[(k - l) * 2 + 1] * xl;
-        }
-        y[2 * e] = a0;
-        y[2 * e + 1] = a1;
+// Toeplitz products over three lanes per output: an output's sum of up to Hb
+// terms is split by term index mod 3 over lanes 3j, 3j+1, 3j+2 of a wave
+// (21 outputs per wave, 84 per pass of the 256 threads) and recombined with
+// two lane shuffles, so the longest serial chain is ceil(Hb / 3) terms and
+// all four waves share the work (one lane per output used 80 of 256 threads
+// with chains of up to Hb terms).  fn(e, sum) runs in the owner lane (s == 0).
+constexpr int kSplit = 3, kPerWave = 21, kPerPass = kPerWave * NWAVE;
+template <class TermSum, class Fn>
+__device__ __forceinline__ void split3_outputs(int nout, TermSum part, Fn fn) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int j = lane / kSplit, sidx = lane - j * kSplit;
+    for (int base = 0; base < nout; base += kPerPass) {
+        const int e = base + w * kPerWave + j;
+        const bool valid = lane < kSplit * kPerWave && e < nout;
+        double2v acc = valid ? part(e, sidx) : double2v{0.0, 0.0};
+        const double x1 = __shfl_down(acc.x, 1), y1 = __shfl_down(acc.y, 1);
+        const double x2 = __shfl_down(acc.x, 2), y2 = __shfl_down(acc.y, 2);
+        if (valid && sidx == 0) fn(e, double2v{acc.x + x1 + x2, acc.y + y1 + y2});
     }
 }
 
-// sum_{k>=l} g[v][k-l]' y[v][k]        (entry of calB' y)
-template <class LT, class PY>
-__device__ __forceinline__ double toeplitz_t_entry(const LT& L, PY y, int v, int l) {
-    const ldouble* gv = L.g + v * L.Hb * 2;
-    const int yb = v * L.Hb * 2;
-    double acc = 0.0;
-    for (int k = l; k < L.Hb; ++k)
-        acc += gv[(k - l) * 2] * y[yb + 2 * k] + gv[(k - l) * 2 + 1] * y[yb + 2 * k + 1];
-    return acc;
+// y[v][k] = sum_{l<=k} g[v][k-l] * x[v*Hb + l]     (calB x, MPC_Iter.py:146-147)
+template <class LT, class PX, class PY>
+__device__ __forceinline__ void toeplitz_apply(const LT& L, PX x, PY y) {
+    split3_outputs(
+        L.V * L.Hb,
+        [&](int e, int sidx) {
+            const int v = e / L.Hb, k = e - v * L.Hb;
+            const ldouble* gv = L.g + v * L.Hb * 2;
+            const int xb = v * L.Hb;
+            double a0 = 0.0, a1 = 0.0;
+            for (int l = sidx; l <= k; l += kSplit) {
+                const double xl = x[xb + l];
+                const double2v gl = ld2(gv + (k - l) * 2);
+                a0 += gl.x * xl;
+                a1 += gl.y * xl;
+            }
+            return double2v{a0, a1};
+        },
+        [&](int e, double2v r) { st2(y + 2 * e, r); });
+}
+
+// out(e, sum_{k>=l} g[v][k-l]' y[v][k]) for every e = v*Hb + l   (calB' y)
+template <class LT, class PY, class Fn>
+__device__ __forceinline__ void toeplitz_t_apply(const LT& L, PY y, Fn out) {
+    split3_outputs(
+        L.V * L.Hb,
+        [&](int e, int sidx) {
+            const int v = e / L.Hb, l = e - v * L.Hb;
+            const ldouble* gv = L.g + v * L.Hb * 2;
+            const int yb = v * L.Hb * 2;
+            double acc = 0.0;
+            for (int k = l + sidx; k < L.Hb; k += kSplit)
+                acc += gv[(k - l) * 2] * y[yb + 2 * k] + gv[(k - l) * 2 + 1] * y[yb + 2 * k + 1];
+            return double2v{acc, 0.0};
+        },
+        [&](int e, double2v r) { out(e, r.x); });
 }
 
 // sum over the rows incident to (v, k) of coef(r) * sigma * e_r  (2-vector)
@@ -804,10 +834,7 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
     for (int r = tid; r < L.m; r += NT) wsum += t[r] * L.rowW[r];
     double red[4] = {wsum, 0.0, 0.0, 0.0};
     block_reduce4<1>(red, 0, L.red);   // barriers: yb visible afterwards
-    for (int e = tid; e < L.N; e += NT) {
-        const int v = e / L.Hb, l = e % L.Hb;
-        out[e] = toeplitz_t_entry(L, L.yb, v, l) + t[L.m + e] - t[L.m + L.N + e];
-    }
+    toeplitz_t_apply(L, L.yb, [&](int e, double tt) { out[e] = tt + t[L.m + e] - t[L.m + L.N + e]; });
     return red[0] - t[L.mc - 1];
 }
 
@@ -918,10 +945,7 @@ __device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
                 L.H[roff(row) + col] = acc;
             }
     }
-    for (int e = tid; e < N; e += NT) {
-        const int v = e / Hb, l = e % Hb;
-        L.H[roff(N) + e] = toeplitz_t_entry(L, L.yb, v, l);
-    }
+    toeplitz_t_apply(L, L.yb, [&](int e, double tt) { L.H[roff(N) + e] = tt; });
     if (tid == 0) L.H[roff(N) + N] = red[0] + d[L.mc - 1] + rho;
     __syncthreads();
 }
@@ -1462,17 +1486,16 @@ __device__ void residuals(const DevParams& P, const LT& L, double (&out)[4]) {
     double red[4] = {mrp, gap, wl, quad};
     block_reduce4<4>(red, 1, L.red);
     double mrd = 0.0, quad2 = 0.0, lin = 0.0;
-    for (int e = tid; e < N; e += NT) {
-        const int v = e / Hb, l = e % Hb;
+    toeplitz_t_apply(L, L.yb, [&](int e, double tt) {
+        const int v = e / Hb;
         const double ze = L.z[e];
         const double pu = 2.0 * u2 * P.R[v] * ze;
-        const double rde = toeplitz_t_entry(L, L.yb, v, l) + pu + L.qs[e] + L.lam[L.m + e] -
-                           L.lam[L.m + N + e];
+        const double rde = tt + pu + L.qs[e] + L.lam[L.m + e] - L.lam[L.m + N + e];
         L.rd[e] = rde;
         mrd = fmax(mrd, fabs(rde));
         quad2 += pu * ze;
         lin += L.qs[e] * ze;
-    }
+    });
     const double rdw = P.slackW + red[2] - L.lam[L.mc - 1];
     if (tid == 0) L.rd[N] = rdw;
     double red2[4] = {mrd, quad2, lin, 0.0};
