@@ -1511,33 +1511,13 @@ template <class LT>
 __device__ double max_step(const LT& L) {
     double a = 1.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
-        if (L.ds[r] < 0.0) a = fmin(a, -L.s[r] / L.ds[r]);
-        if (L.dl[r] < 0.0) a = fmin(a, -L.lam[r] / L.dl[r]);
+        // v_rcp_f64 + Newton instead of the IEEE division sequence (per row, every step)
+        if (L.ds[r] < 0.0) a = fmin(a, -L.s[r] * recip(L.ds[r]));
+        if (L.dl[r] < 0.0) a = fmin(a, -L.lam[r] * recip(L.dl[r]));
     }
     double red[4] = {-a, 0.0, 0.0, 0.0};
     block_reduce4<1>(red, 1, L.red);
     return -red[0];
-}
-
-// Newton direction for complementarity target rc (rc_of(r)):
-//   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
-template <class LT, class RC>
-__device__ void newton_dir(const LT& L, RC rc_of) {
-    for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.dd[r] * L.rp[r] - rc_of(r) / L.s[r];
-    __syncthreads();
-    const double ow = gt_apply(L, L.tv, L.rhs);
-    if (threadIdx.x == 0) L.rhs[L.N] = ow;
-    __syncthreads();
-    for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
-    __syncthreads();
-    chol_solve(L, L.rhs, L.dz);
-    g_apply(L, L.dz, L.ds, false);
-    for (int r = threadIdx.x; r < L.mc; r += NT) {
-        const double dsr = -L.rp[r] - L.ds[r];
-        L.ds[r] = dsr;
-        L.dl[r] = -(rc_of(r) + L.lam[r] * dsr) / L.s[r];
-    }
-    __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -1641,7 +1621,7 @@ PHASE void ph_init_b(Ctx c) {
 }
 PHASE void ph_scaling(Ctx c) {
     LAYDEF;
-    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] / L.s[r];
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
     __syncthreads();
 }
 // Newton direction, complementarity target rc = s lam (+ ds_aff dl_aff - smu if corr):
@@ -1650,7 +1630,7 @@ PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
     LAYDEF;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
-        L.tv[r] = L.dd[r] * L.rp[r] - rc / L.s[r];
+        L.tv[r] = L.dd[r] * L.rp[r] - rc * recip(L.s[r]);
     }
     __syncthreads();
     const double ow = gt_apply(L, L.tv, L.rhs);
@@ -1666,7 +1646,7 @@ PHASE void ph_newton_back(Ctx c, int corr, double smu) {
         const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
         const double dsr = -L.rp[r] - L.ds[r];
         L.ds[r] = dsr;
-        L.dl[r] = -(rc + L.lam[r] * dsr) / L.s[r];
+        L.dl[r] = -(rc + L.lam[r] * dsr) * recip(L.s[r]);
     }
     __syncthreads();
 }
