@@ -1619,15 +1619,15 @@ PHASE void ph_init_b(Ctx c) {
     }
     __syncthreads();
 }
-PHASE void ph_scaling(Ctx c) {
-    LAYDEF;
-    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
-    __syncthreads();
-}
+// Interior-point step bodies.  The phase functions below chain several of
+// them in one out-of-line call: every call costs its register save/restore
+// and layout rebuild (~2k cycles for a trivial phase), and the bodies of one
+// chain touch the same rows from the same threads.
+//
 // Newton direction, complementarity target rc = s lam (+ ds_aff dl_aff - smu if corr):
 //   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
-PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ void newton_rhs_body(const LT& L, int corr, double smu) {
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
         L.tv[r] = L.dd[r] * L.rp[r] - rc * recip(L.s[r]);
@@ -1639,8 +1639,8 @@ PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
     for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
     __syncthreads();
 }
-PHASE void ph_newton_back(Ctx c, int corr, double smu) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ void newton_back_body(const LT& L, int corr, double smu) {
     g_apply(L, L.dz, L.ds, false);
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
@@ -1651,8 +1651,8 @@ PHASE void ph_newton_back(Ctx c, int corr, double smu) {
     __syncthreads();
 }
 // predictor step length and Mehrotra centring: returns sigma * mu; stores the affine direction
-PHASE double ph_affine(Ctx c, double mu) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ double affine_body(const LT& L, double mu) {
     const double aaff = max_step(L);
     double mua = 0.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
@@ -1665,8 +1665,8 @@ PHASE double ph_affine(Ctx c, double mu) {
     const double sr = red[0] / L.mc / mu;
     return sr * sr * sr * mu;
 }
-PHASE void ph_update(Ctx c) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ void update_body(const LT& L) {
     const double alpha = fmin(1.0, 0.99 * max_step(L));
     for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] += alpha * L.dz[e];
     for (int r = threadIdx.x; r < L.mc; r += NT) {
@@ -1674,6 +1674,32 @@ PHASE void ph_update(Ctx c) {
         L.lam[r] += alpha * L.dl[r];
     }
     __syncthreads();
+}
+// d = lam / s, then K = P + G' diag(d) G
+PHASE void ph_scale_assemble(Ctx c) {
+    LAYDEF;
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
+    __syncthreads();
+    assemble(P, L, L.dd, 0.0);
+}
+// predictor right-hand side (rc = s lam)
+PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
+    LAYDEF;
+    newton_rhs_body(L, corr, smu);
+}
+// predictor back-substitution, affine step and centring, corrector right-hand side
+PHASE double ph_back_affine_rhs(Ctx c, double mu) {
+    LAYDEF;
+    newton_back_body(L, 0, 0.0);
+    const double smu = affine_body(L, mu);
+    newton_rhs_body(L, 1, smu);
+    return smu;
+}
+// corrector back-substitution and the damped step
+PHASE void ph_back_update(Ctx c, double smu) {
+    LAYDEF;
+    newton_back_body(L, 1, smu);
+    update_body(L);
 }
 // polish: weights 1/delta on the active set {lam > s}, y = lam there, x_0 = z
 PHASE void ph_polish_prep(Ctx c) {
@@ -1899,8 +1925,7 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
             break;
         }
         const double mu = res.c / mc;
-        PH(ph_scaling)(c);
-        PH(ph_assemble)(c, 0.0);
+        PH(ph_scale_assemble)(c);
         PROF_ACC(2);
         if (!PH(ph_cholesky)(c)) break;
         PROF_ACC(3);
@@ -1908,14 +1933,11 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
         PROF_ACC(4);
         PH(ph_solve)(c, 1);
         PROF_ACC(9);
-        PH(ph_newton_back)(c, 0, 0.0);
-        const double smu = PH(ph_affine)(c, mu);
-        PH(ph_newton_rhs)(c, 1, smu);
+        const double smu = PH(ph_back_affine_rhs)(c, mu);
         PROF_ACC(5);
         PH(ph_solve)(c, 1);
         PROF_ACC(9);
-        PH(ph_newton_back)(c, 1, smu);
-        PH(ph_update)(c);
+        PH(ph_back_update)(c, smu);
         PROF_ACC(6);
     }
     st.ipm += it;
