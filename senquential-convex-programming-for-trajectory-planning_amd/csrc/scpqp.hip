@@ -1535,6 +1535,18 @@ struct D4 {
     double a, b, c, d;
 };
 
+// Multiplier-iteration stopping rule of the polish (oracle POLISH_TOL): 1 once
+// x stops moving (|dx| <= tol max(1, |x|)), 2 when the iterate shows the active
+// set is wrong (warm rounds: a violated inactive row or a negative active
+// multiplier beyond `early`), 0 to continue.  Never before the second solve.
+constexpr double kPolishTol = 1e-10;
+__device__ __forceinline__ int polish_stop(const D4& d, int ref, double early) {
+    if (ref < 1) return 0;
+    if (d.a <= kPolishTol * fmax(1.0, d.b)) return 1;
+    if (d.c > early || d.d > early) return 2;
+    return 0;
+}
+
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
     const Off f = plan_offsets(c.P->nV, c.P->nO, c.P->hpMax, HG, VG);
@@ -1575,13 +1587,17 @@ PHASE D4 ph_residuals(Ctx c) {
     return D4{r[0], r[1], r[2], r[3]};
 }
 // rhs = -q + G'(tv) with tv = h (init) or tv = mask (h/delta - y) (polish), + rho x_k
-PHASE void ph_rhs_from_tv(Ctx c, double rho) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ void rhs_from_tv_body(const DevParams& P, const LT& L, double rho) {
     const double ow = gt_apply(L, L.tv, L.rhs);
     if (threadIdx.x == 0) L.rhs[L.N] = ow - P.slackW + rho * L.dz[L.N];
     __syncthreads();
     for (int e = threadIdx.x; e < L.N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
     __syncthreads();
+}
+PHASE void ph_rhs_from_tv(Ctx c, double rho) {
+    LAYDEF;
+    rhs_from_tv_body(P, L, rho);
 }
 // initial-point setup of dd/tv/dz
 PHASE void ph_init_a(Ctx c) {
@@ -1675,17 +1691,14 @@ __device__ __forceinline__ void update_body(const LT& L) {
     }
     __syncthreads();
 }
-// d = lam / s, then K = P + G' diag(d) G
-PHASE void ph_scale_assemble(Ctx c) {
+// d = lam / s, K = P + G' diag(d) G, and the predictor right-hand side (rc = s lam;
+// it does not need the factor, so it is formed before the factorisation)
+PHASE void ph_scale_assemble_rhs(Ctx c) {
     LAYDEF;
     for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
     __syncthreads();
     assemble(P, L, L.dd, 0.0);
-}
-// predictor right-hand side (rc = s lam)
-PHASE void ph_newton_rhs(Ctx c, int corr, double smu) {
-    LAYDEF;
-    newton_rhs_body(L, corr, smu);
+    newton_rhs_body(L, 0, 0.0);
 }
 // predictor back-substitution, affine step and centring, corrector right-hand side
 PHASE double ph_back_affine_rhs(Ctx c, double mu) {
@@ -1695,11 +1708,15 @@ PHASE double ph_back_affine_rhs(Ctx c, double mu) {
     newton_rhs_body(L, 1, smu);
     return smu;
 }
-// corrector back-substitution and the damped step
-PHASE void ph_back_update(Ctx c, double smu) {
+// corrector back-substitution, the damped step, and the residuals of the new
+// point (the next iteration's convergence test)
+PHASE D4 ph_back_update_residuals(Ctx c, double smu) {
     LAYDEF;
     newton_back_body(L, 1, smu);
     update_body(L);
+    double r[4];
+    residuals(P, L, r);
+    return D4{r[0], r[1], r[2], r[3]};
 }
 // polish: weights 1/delta on the active set {lam > s}, y = lam there, x_0 = z
 PHASE void ph_polish_prep(Ctx c) {
@@ -1735,17 +1752,23 @@ PHASE D4 ph_scales(Ctx c) {
     block_reduce4<2>(red, 3, L.red);
     return D4{red[0], red[1], 0.0, 0.0};
 }
-PHASE void ph_polish_tv(Ctx c) {
-    LAYDEF;
+// polish right-hand side: tv = mask (h / delta - y), rhs = -q + G' tv + rho x_k
+template <class LT>
+__device__ __forceinline__ void polish_rhs_body(const DevParams& P, const LT& L) {
     const double idl = 1.0 / P.polDelta;
     for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
     __syncthreads();
+    rhs_from_tv_body(P, L, P.polRho);
+}
+PHASE void ph_polish_rhs(Ctx c) {
+    LAYDEF;
+    polish_rhs_body(P, L);
 }
 // rp = G x_k - h;  y += rp / delta on the active set.  Returns
 // {max |x_k - x_{k-1}|, max |x_k|, max rp over the inactive rows, -min y over
 // the active rows} (x_{k-1} kept in rd, dead during the polish).
-PHASE D4 ph_polish_dual(Ctx c) {
-    LAYDEF;
+template <class LT>
+__device__ __forceinline__ D4 polish_dual_body(const DevParams& P, const LT& L) {
     const double idl = 1.0 / P.polDelta;
     g_apply(L, L.dz, L.rp, true);
     double viol = -1e300, yneg = -1e300;
@@ -1768,6 +1791,14 @@ PHASE D4 ph_polish_dual(Ctx c) {
     double red[4] = {dmax, xmax, viol, yneg};
     block_reduce4<4>(red, 15, L.red);
     return D4{red[0], red[1], red[2], red[3]};
+}
+// the multiplier update, and, unless the caller's stopping rule (polish_stop)
+// ends the refinement here, the next right-hand side in the same call
+PHASE D4 ph_polish_dual_next(Ctx c, int ref, int cap, double early) {
+    LAYDEF;
+    const D4 d = polish_dual_body(P, L);
+    if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
+    return d;
 }
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
 // Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
@@ -1828,7 +1859,6 @@ PHASE void ph_take_u(Ctx c) {
 constexpr int kPolishRounds = 6;
 constexpr int kWarmRounds = 8;
 constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: P.nRefine)
-constexpr double kPolishTol = 1e-10;
 // Warm rounds stop refining as soon as the iterate shows the active set is
 // wrong (an inactive row violated, or an active multiplier negative, by more
 // than this in scaled units): the correction comes earlier and the refinement
@@ -1862,17 +1892,14 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds
             if (!fact) break;
         }
         int conv = 0;
+        PH(ph_polish_rhs)(c);
         for (int ref = 0; ref < cap; ++ref) {
-            PH(ph_polish_tv)(c);
-            PH(ph_rhs_from_tv)(c, P.polRho);
             PH(ph_solve)(c, 1);
-            const D4 d = PH(ph_polish_dual)(c);
+            const D4 d = PH(ph_polish_dual_next)(c, ref, cap, early);
             ++st.refine;
-            if (ref >= 1 && d.a <= kPolishTol * fmax(1.0, d.b)) {
-                conv = 1;
-                break;
-            }
-            if (ref >= 1 && (d.c > early || d.d > early)) break;
+            const int stop = polish_stop(d, ref, early);
+            conv = stop == 1;
+            if (stop) break;
         }
         const int acc = PH(ph_polish_accept)(c, hmax, conv);
         PROF_ACC(8);
@@ -1915,29 +1942,27 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
     // ---- Mehrotra iterations
     int it = 0;
     bool conv = false;
+    D4 res = PH(ph_residuals)(c);
+    PROF_ACC(1);
     for (; it < P.maxIpm; ++it) {
         PROF_ACC(0);
-        const D4 res = PH(ph_residuals)(c);
-        PROF_ACC(1);
         if (res.a <= P.ipmTol * hmax && res.b <= P.ipmTol * qmax &&
             res.c <= P.ipmTol * fmax(1.0, fabs(res.d))) {
             conv = true;
             break;
         }
         const double mu = res.c / mc;
-        PH(ph_scale_assemble)(c);
+        PH(ph_scale_assemble_rhs)(c);
         PROF_ACC(2);
         if (!PH(ph_cholesky)(c)) break;
         PROF_ACC(3);
-        PH(ph_newton_rhs)(c, 0, 0.0);
-        PROF_ACC(4);
         PH(ph_solve)(c, 1);
         PROF_ACC(9);
         const double smu = PH(ph_back_affine_rhs)(c, mu);
         PROF_ACC(5);
         PH(ph_solve)(c, 1);
         PROF_ACC(9);
-        PH(ph_back_update)(c, smu);
+        res = PH(ph_back_update_residuals)(c, smu);
         PROF_ACC(6);
     }
     st.ipm += it;

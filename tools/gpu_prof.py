@@ -12,8 +12,8 @@ lib.scpqp_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 from oracle import scp_reference as R
 from scpqp import batch as BT
 from scpqp.solver import ScpQpSolver
-names = ["ipm-loop-top", "residuals", "assemble", "cholesky", "newton(pred)", "maxstep+corr",
-         "update", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
+names = ["ipm-loop-top", "residuals(first)", "scale+assemble+rhs", "cholesky", "(unused)", "back+affine+corr-rhs",
+         "back+update+residuals", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
          "chol:panel0", "chol:steps", "solve:fwd", "solve:bwd",   # 12-15: sub-phases of 3 / 9
          "ipm-init", "take_u+evaluate",
          "panel:load", "panel:lookahead", "panel:pivots", "panel:store", "barrier-wait(w0)", "barrier-wait(w1)"]
