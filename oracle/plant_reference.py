@@ -168,6 +168,23 @@ def evaluate_in_original_problem(sc, U, traj, ref_points, obst_future=None,
                 constraintValuesObstacle=co, predictionFeasible=feasible)
 
 
+def obstacle_state(sc, tick):
+    """obstaclePathFullRes[:, :, tick] (main.py:61-71): constant-velocity obstacles."""
+    out = np.zeros((sc.nObst, 2))
+    for o, ob in enumerate(sc.obstacles):
+        out[o, 0] = (tick * sc.tick_length) * ob[3] * math.cos(ob[2]) + ob[0]
+        out[o, 1] = (tick * sc.tick_length) * ob[3] * math.sin(ob[2]) + ob[1]
+    return out
+
+
+def obstacle_prediction(sc, tick_meas):
+    """Iter.obstacleFutureTrajectories [nObst, 2, Hp] of an MPC step (MPC_Iter.py:45-51)
+    from the obstacle state at the measurement tick (main.py:123)."""
+    if not sc.nObst:
+        return np.zeros((0, 2, sc.Hp))
+    return R.obstacle_future(sc, obstacle_state(sc, tick_meas), sc.Hp)
+
+
 class ClosedLoop:
     """Restatement of ``Simulation.runsimulation`` (main.py:98-206) for one
     realisation with the SCP controller of ``scp_reference`` (structured mode).
@@ -199,7 +216,8 @@ class ClosedLoop:
         lo = max(sc.ticks_delay_x - tick_now, 0)
         u_path[:, lo:lo + tick_act - 1 - tick_meas] = self.control[:, tick_meas + 1:tick_act]
         x0, u0, dtraj = delay_compensate(sc, x_meas, u_path[:, -1])
-        p = R.make_problem(sc, x0, u0, np.zeros((nV, 2)), Hp=sc.Hp)
+        obst = obstacle_prediction(sc, tick_meas)
+        p = R.make_problem(sc, x0, u0, np.zeros((nV, 2)), Hp=sc.Hp, obst=obst)
         res = R.scp_solve(p, u_warm=self.u_prev, mode="structured")
         self.u_prev = res.u.copy()
         U = clip_controls(res.U, u0, umax, self.du_lim)
@@ -211,7 +229,8 @@ class ClosedLoop:
             u_of_k = [self.control[v, control_tick_index(sc, t)] for t in timelist]
             ms = plant_step(sc, v, self.path[:, v, tick_now], i * sc.dt, u_of_k)
             self.path[:, v, tps * i + 1:tps * (i + 1) + 1] = ms[1:].T
-        ev = evaluate_in_original_problem(sc, U, res.traj, p.ref_points)
+        ev = evaluate_in_original_problem(sc, U, res.traj, p.ref_points,
+                                          obst if sc.nObst else None)
         self.records.append(dict(x0=x0, u0=u0, delay_traj=dtraj, umax=umax, U=U, traj=res.traj,
                                  n_scp=res.n_scp, u=res.u, evaluation=ev))
         return self.records[-1]

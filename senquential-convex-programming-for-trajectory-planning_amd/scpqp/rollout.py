@@ -99,8 +99,9 @@ class ClosedLoopBatch:
         self.h_max = h_max
         self.keep_path = keep_path
         self.evaluate = evaluate
-        if scenario.nObst:
-            raise ValueError("obstacle scenarios: the batched rollout covers nObst = 0")
+        self.nO = int(scenario.nObst)
+        self.obstacles = np.asarray(scenario.obstacles, float).reshape(self.nO, -1) if self.nO \
+            else np.zeros((0, 6))
         self.params = PL.plant_params(scenario.Lf, scenario.Lr)
         self.solver = ScpQpSolver(scenario, max_batch=self.B, device=self.device, **solver_kw)
         self.du_lim = float(scenario.mechanicalSteeringLimit) * 2          # Scenarios.py:50
@@ -131,6 +132,24 @@ class ClosedLoopBatch:
         self.history = []
         self.i = 0
 
+    def _obstacle_prediction(self, tick_meas):
+        """Iter.obstacleFutureTrajectories (MPC_Iter.py:45-51) from the constant-velocity
+        obstacle state at the measurement tick (main.py:61-71, 123); the same for every
+        realisation.  Returns a device tensor [B, nObst, 2, Hp] or None."""
+        if not self.nO:
+            return None
+        sc, ob = self.sc, self.obstacles
+        t_meas = tick_meas * sc.tick_length
+        x = t_meas * ob[:, 3] * np.cos(ob[:, 2]) + ob[:, 0]
+        y = t_meas * ob[:, 3] * np.sin(ob[:, 2]) + ob[:, 1]
+        lead = sc.delay_x + sc.dt + sc.delay_u
+        step = ((np.arange(self.Hp) + 1) * sc.dt + lead)[None, :] * ob[:, 3:4]   # [nO, Hp]
+        fut = np.zeros((self.nO, 2, self.Hp))
+        fut[:, 0] = step * np.cos(ob[:, 2:3]) + x[:, None]
+        fut[:, 1] = step * np.sin(ob[:, 2:3]) + y[:, None]
+        t = torch.as_tensor(fut, dtype=torch.float64, device=self.device)
+        return t[None].expand(self.B, -1, -1, -1).contiguous()
+
     def _held_command(self, tick_now):
         return held_command_tick(tick_now, self.tdx, self.tdu, self.tps, self.ticks_total)
 
@@ -153,7 +172,8 @@ class ClosedLoopBatch:
         x0, dtraj = PL.delay_compensate(self.params, x_meas.contiguous(), u_hold, horizon,
                                         noise=self.noise, h_max=self.h_max, device=self.device)
         # SCP solve, warm-started from the previous controller output (SCP_controller.py:42-43)
-        out = self.solver.solve(x0, u_hold, u_warm=self.u_prev, out=self.out)
+        obst = self._obstacle_prediction(max(0, tick_now - self.tdx))
+        out = self.solver.solve(x0, u_hold, u_warm=self.u_prev, obst=obst, out=self.out)
         self.u_prev = out.u.clone()
         U = out.u.clone()
         PL.clip_controls(U, u_hold, umax, nV, Hp, self.du_lim)
@@ -177,7 +197,7 @@ class ClosedLoopBatch:
             # main.py:201-202: evaluateInOriginalProblem on the clipped U and the prediction
             ref = self.solver.sample_reference(x0)
             rec["evaluation"] = evaluate_in_original_problem(
-                sc, U.view(B, nV, Hp).transpose(1, 2), rec["traj"], ref)
+                sc, U.view(B, nV, Hp).transpose(1, 2), rec["traj"], ref, obst)
         if self.keep_path:
             rec["path"] = path
             rec["delay_traj"] = dtraj

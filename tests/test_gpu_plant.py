@@ -167,3 +167,37 @@ def test_dropin_delay_compensation_matches_straight_line_and_odeint(gpu):
     assert np.abs(traj - tr).max() < 1e-6 and np.allclose(u0[:, 0], u_path[:, -1])
     with pytest.raises(AssertionError):
         MPC_Iter.delay_compensate(sc, x_meas, np.zeros((4, nT + 1)))
+
+
+@pytest.mark.parametrize("kind", ["frog", "parallel5"])
+def test_closed_loop_rollout_with_obstacles(gpu, kind):
+    """Closed loop on the obstacle scenarios (Scenarios.py:127-201): obstacle
+    predictions from the constant-velocity obstacle paths (main.py:61-71,
+    MPC_Iter.py:45-51) feed the solve and the evaluation."""
+    from scpqp.rollout import ClosedLoopBatch
+    sc = R.frog_scenario(Hp=10) if kind == "frog" else R.parallel_scenario(5, Hp=10)
+    rng = np.random.default_rng(3)
+    B, steps, nV = 2, 2, sc.nVeh
+    x_init = np.array(sc.x0)[None] + rng.normal(0, 1, (B, nV, 6)) * np.array(
+        [0.05, 0.05, 0.005, 0.02, 0, 0.002])
+    cl = ClosedLoopBatch(sc, B, device=gpu, keep_path=True)
+    cl.reset(x_init)
+    hist = cl.run(steps)
+    compared = 0
+    for b in range(B):
+        ref = PR.ClosedLoop(sc, x_init=x_init[b])
+        for i in range(steps):
+            r = ref.step(i)
+            h = hist[i]
+            assert np.abs(h["x0"][b].cpu().numpy() - r["x0"]).max() < 1e-6
+            if int(h["n_scp"][b]) != r["n_scp"]:
+                break
+            compared += 1
+            U = h["U"][b].cpu().numpy().reshape(nV, 10).T
+            assert np.abs(U - r["U"]).max() < 1e-6
+            ev, rev = h["evaluation"], r["evaluation"]
+            assert bool(ev["predictionFeasible"][b]) == rev["predictionFeasible"]
+            assert np.abs(ev["constraintValuesObstacle"][b].cpu().numpy()
+                          - rev["constraintValuesObstacle"]).max() < 1e-6
+    assert compared >= 2
+    cl.close()
