@@ -232,5 +232,33 @@ class ClosedLoop:
         ev = evaluate_in_original_problem(sc, U, res.traj, p.ref_points,
                                           obst if sc.nObst else None)
         self.records.append(dict(x0=x0, u0=u0, delay_traj=dtraj, umax=umax, U=U, traj=res.traj,
-                                 n_scp=res.n_scp, u=res.u, evaluation=ev))
+                                 n_scp=res.n_scp, u=res.u, evaluation=ev, ref=p.ref_points))
         return self.records[-1]
+
+    def result_for_plot(self):
+        """``result_for_plot1`` of main.py:213-225 (the JSON draw_video.py:44-56 reads),
+        as numpy arrays, over the steps run so far; timing fields are zero."""
+        sc = self.sc
+        nV, Hp, Nsim = sc.nVeh, sc.Hp, sc.Nsim
+        out = dict(
+            vehiclePathFullRes=self.path.copy(),
+            obstaclePathFullRes=np.stack([obstacle_state(sc, t) for t in range(sc.ticks_total + 1)],
+                                         axis=-1) if sc.nObst
+            else np.zeros((0, 2, sc.ticks_total + 1)),
+            controlPathFullRes=self.control.copy(),
+            controlPredictions=np.zeros((Hp, nV, Nsim)),
+            trajectoryPredictions=np.zeros((Hp, 2, nV, Nsim)),
+            initial_pos=np.zeros((2, nV, Nsim)),
+            ReferenceTrajectory=np.zeros((Hp, 2, nV, Nsim)),
+            MPC_delay_compensation_trajectory=np.zeros((DELAY_STEPS, NX, nV, Nsim)),
+            evaluations_obj_value=[float(r["evaluation"]["predictionObjectiveValue"])
+                                   for r in self.records],
+            controllerRuntime=np.zeros((Nsim, 1)),
+            stepTime=np.zeros((Nsim, 1)))
+        for i, r in enumerate(self.records):
+            out["controlPredictions"][:, :, i] = r["U"]
+            out["trajectoryPredictions"][:, :, :, i] = r["traj"]
+            out["initial_pos"][:, :, i] = r["x0"][:, 0:2].T
+            out["ReferenceTrajectory"][:, :, :, i] = r["ref"]
+            out["MPC_delay_compensation_trajectory"][:, :, :, i] = r["delay_traj"]
+        return out

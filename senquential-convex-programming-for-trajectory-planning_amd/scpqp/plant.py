@@ -20,6 +20,7 @@ from . import _lib as LB
 
 H_MAX = 2.5e-3
 STEER_TAU = 0.1       # Model.py:83: dx[5] = (u_ref - u) / 0.1
+DELAY_STEPS = 10      # MPC_Iter.py:21: outputs of the delay-compensation trajectory
 
 
 def plant_params(lf, lr):
@@ -48,7 +49,7 @@ def _stream(device):
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
 
-def delay_compensate(params, x_meas, u_hold, horizon, n_out=10, noise=None, h_max=H_MAX,
+def delay_compensate(params, x_meas, u_hold, horizon, n_out=DELAY_STEPS, noise=None, h_max=H_MAX,
                      device=None, want_traj=True):
     """x_meas [B, nVeh, 6], u_hold [B, nVeh] -> (x0 [B, nVeh, 6],
     traj [B, n_out, 6, nVeh] or None): MPC_Iter.py:24-33 for every problem."""

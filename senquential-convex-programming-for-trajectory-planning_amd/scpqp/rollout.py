@@ -21,7 +21,9 @@ initial state (and optional constant model-noise terms).
 """
 from __future__ import annotations
 
+import json
 import math
+import time
 
 import numpy as np
 import torch
@@ -86,7 +88,7 @@ def held_command_tick(tick_now, tdx, tdu, tps, ticks_total):
 
 class ClosedLoopBatch:
     def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, evaluate=True,
-                 **solver_kw):
+                 timing=False, **solver_kw):
         self.sc = scenario
         self.B = int(B)
         self.device = torch.device(device or "cuda")
@@ -99,6 +101,7 @@ class ClosedLoopBatch:
         self.h_max = h_max
         self.keep_path = keep_path
         self.evaluate = evaluate
+        self.timing = timing
         self.nO = int(scenario.nObst)
         self.obstacles = np.asarray(scenario.obstacles, float).reshape(self.nO, -1) if self.nO \
             else np.zeros((0, 6))
@@ -122,6 +125,7 @@ class ClosedLoopBatch:
         if tuple(x.shape) != (self.B, self.nV, 6):
             raise ValueError("x_init must be [B, nVeh, 6]")
         self.state.copy_(x)
+        self.x_init = x.clone()
         self.control.fill_(float("nan"))
         u0 = torch.tensor([float(u) for u in self.sc.u0], dtype=torch.float64, device=self.device)
         self.control[:, :, 0:self.tdu + self.tps + 1] = u0[None, :, None]
@@ -156,6 +160,9 @@ class ClosedLoopBatch:
     def step(self):
         i, sc, B, nV, Hp, tps = self.i, self.sc, self.B, self.nV, self.Hp, self.tps
         f = dict(dtype=torch.float64, device=self.device)
+        if self.timing:
+            torch.cuda.synchronize(self.device)
+        t_step = time.perf_counter()
         tick_now = i * tps
         # measured state: tick_now - ticks_delay_x (inside the previous step's path)
         if self.tdx == 0 or self.last_path is None:
@@ -175,6 +182,9 @@ class ClosedLoopBatch:
         obst = self._obstacle_prediction(max(0, tick_now - self.tdx))
         out = self.solver.solve(x0, u_hold, u_warm=self.u_prev, obst=obst, out=self.out)
         self.u_prev = out.u.clone()
+        if self.timing:
+            torch.cuda.synchronize(self.device)
+        t_ctrl = time.perf_counter() - t_step
         U = out.u.clone()
         PL.clip_controls(U, u_hold, umax, nV, Hp, self.du_lim)
         # actuator-delayed control path (main.py:176-182)
@@ -196,11 +206,16 @@ class ClosedLoopBatch:
         if self.evaluate:
             # main.py:201-202: evaluateInOriginalProblem on the clipped U and the prediction
             ref = self.solver.sample_reference(x0)
+            rec["ref"] = ref
             rec["evaluation"] = evaluate_in_original_problem(
                 sc, U.view(B, nV, Hp).transpose(1, 2), rec["traj"], ref, obst)
         if self.keep_path:
             rec["path"] = path
             rec["delay_traj"] = dtraj
+        if self.timing:
+            torch.cuda.synchronize(self.device)
+        rec["controllerRuntime"] = t_ctrl               # batch latency: every realisation
+        rec["stepTime"] = time.perf_counter() - t_step   # of the batch shares it
         self.history.append(rec)
         self.i += 1
         return rec
@@ -209,6 +224,54 @@ class ClosedLoopBatch:
         for _ in range(n_steps):
             self.step()
         return self.history
+
+    def result_for_plot(self, b):
+        """``result_for_plot1`` of main.py:213-225 for realisation b, the dict
+        draw_video.py:44-56 reads back, as numpy arrays over the steps run so far
+        (needs keep_path=True and evaluate=True).  Unset path ticks stay NaN and
+        unrun steps zero, as main.py initialises them (main.py:56-62).  Timing fields
+        are the batch's per-step wall times (meaningful with timing=True)."""
+        if not self.keep_path or not self.evaluate:
+            raise ValueError("result_for_plot needs keep_path=True and evaluate=True")
+        sc, nV, Hp, tps = self.sc, self.nV, self.Hp, self.tps
+        Nsim, T = int(sc.Nsim), self.ticks_total
+        veh = np.full((6, nV, T + 1), np.nan)
+        veh[:, :, 0] = self.x_init[b].cpu().numpy().T
+        obs = np.zeros((self.nO, 2, T + 1))
+        if self.nO:
+            t = np.arange(T + 1) * sc.tick_length                       # main.py:61-71
+            ob = self.obstacles
+            obs[:, 0] = t[None] * (ob[:, 3] * np.cos(ob[:, 2]))[:, None] + ob[:, 0:1]
+            obs[:, 1] = t[None] * (ob[:, 3] * np.sin(ob[:, 2]))[:, None] + ob[:, 1:2]
+        out = dict(
+            vehiclePathFullRes=veh, obstaclePathFullRes=obs,
+            controlPathFullRes=self.control[b].cpu().numpy(),
+            controlPredictions=np.zeros((Hp, nV, Nsim)),
+            trajectoryPredictions=np.zeros((Hp, 2, nV, Nsim)),
+            initial_pos=np.zeros((2, nV, Nsim)),
+            ReferenceTrajectory=np.zeros((Hp, 2, nV, Nsim)),
+            MPC_delay_compensation_trajectory=np.zeros((PL.DELAY_STEPS, 6, nV, Nsim)),
+            evaluations_obj_value=[float(r["evaluation"]["predictionObjectiveValue"][b])
+                                   for r in self.history],
+            controllerRuntime=np.zeros((Nsim, 1)), stepTime=np.zeros((Nsim, 1)))
+        for i, r in enumerate(self.history[:Nsim]):
+            lo = tps * i + 1
+            hi = min(T + 1, tps * (i + 1) + 1)
+            veh[:, :, lo:hi] = r["path"][b, :, 1:1 + hi - lo].cpu().numpy().transpose(2, 0, 1)
+            out["controlPredictions"][:, :, i] = r["U"][b].view(nV, Hp).T.cpu().numpy()
+            out["trajectoryPredictions"][:, :, :, i] = r["traj"][b].cpu().numpy()
+            out["initial_pos"][:, :, i] = r["x0"][b, :, 0:2].T.cpu().numpy()
+            out["ReferenceTrajectory"][:, :, :, i] = r["ref"][b].cpu().numpy()
+            out["MPC_delay_compensation_trajectory"][:, :, :, i] = r["delay_traj"][b].cpu().numpy()
+            out["controllerRuntime"][i, 0] = r["controllerRuntime"]
+            out["stepTime"][i, 0] = r["stepTime"]
+        return out
+
+    def dump_result(self, fp, b):
+        """json.dump of result_for_plot(b) with main.py:226-231's encoding (nested
+        lists, NaN written as NaN)."""
+        res = self.result_for_plot(b)
+        json.dump({k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in res.items()}, fp)
 
     def close(self):
         self.solver.close()

@@ -201,3 +201,47 @@ def test_closed_loop_rollout_with_obstacles(gpu, kind):
                           - rev["constraintValuesObstacle"]).max() < 1e-6
     assert compared >= 2
     cl.close()
+
+
+def test_result_for_plot_matches_restatement(gpu, tmp_path):
+    """f3 at batch scale: ClosedLoopBatch.result_for_plot(b) (main.py:213-225's
+    result_for_plot1) against the restatement's, field by field, and dump_result
+    readable by json with draw_video.py:44-56's reshapes."""
+    import json
+    from scpqp.rollout import ClosedLoopBatch
+    sc = R.frog_scenario(Hp=10)
+    rng = np.random.default_rng(11)
+    B, steps, nV = 2, 2, sc.nVeh
+    x_init = np.array(sc.x0)[None] + rng.normal(0, 1, (B, nV, 6)) * np.array(
+        [0.05, 0.05, 0.005, 0.02, 0, 0.002])
+    cl = ClosedLoopBatch(sc, B, device=gpu, keep_path=True, timing=True)
+    cl.reset(x_init)
+    cl.run(steps)
+    compared = 0
+    for b in range(B):
+        ref = PR.ClosedLoop(sc, x_init=x_init[b])
+        for i in range(steps):
+            ref.step(i)
+        if [int(h["n_scp"][b]) for h in cl.history] != [r["n_scp"] for r in ref.records]:
+            continue
+        compared += 1
+        got, want = cl.result_for_plot(b), ref.result_for_plot()
+        assert set(got) == set(want)
+        tol = dict(vehiclePathFullRes=1e-5, obstaclePathFullRes=1e-12, controlPathFullRes=1e-6,
+                   controlPredictions=1e-6, trajectoryPredictions=1e-5, initial_pos=1e-6,
+                   ReferenceTrajectory=1e-6, MPC_delay_compensation_trajectory=1e-6)
+        for k, t in tol.items():
+            g, w = np.asarray(got[k]), np.asarray(want[k])
+            assert g.shape == w.shape, k
+            assert np.array_equal(np.isnan(g), np.isnan(w)), k
+            assert np.nanmax(np.abs(g - w)) < t, k
+        assert np.allclose(got["evaluations_obj_value"], want["evaluations_obj_value"], rtol=1e-6)
+        assert np.all(got["stepTime"][:steps] > 0) and np.all(got["stepTime"][steps:] == 0)
+        p = tmp_path / f"frog_{b}.json"
+        with open(p, "w") as fp:
+            cl.dump_result(fp, b)
+        back = json.load(open(p))
+        veh = np.reshape(back["vehiclePathFullRes"], (6, nV, sc.ticks_total + 1), order="F")
+        assert np.array_equal(veh, got["vehiclePathFullRes"], equal_nan=True)
+    assert compared >= 1
+    cl.close()

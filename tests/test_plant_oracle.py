@@ -153,3 +153,34 @@ def test_held_command_tick_matches_main_py_slicing(tdx):
         else:
             assert u_path[-1] == control[k]
     assert truncated >= 1            # the last MPC step of main.py holds u = 0
+
+
+@pytest.mark.slow
+def test_result_for_plot_has_main_py_schema():
+    """oracle ClosedLoop.result_for_plot: the keys, shapes and NaN/zero fill of
+    main.py:213-225, round-tripped through json and read back with
+    draw_video.py:44-56's reshapes."""
+    import json
+    sc = R.frog_scenario(Hp=10)
+    cl = PR.ClosedLoop(sc)
+    cl.step(0)
+    res = cl.result_for_plot()
+    nV, Hp, Nsim, T = sc.nVeh, sc.Hp, sc.Nsim, sc.ticks_total
+    txt = json.dumps({k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in res.items()})
+    back = json.loads(txt)
+    shapes = dict(vehiclePathFullRes=(6, nV, T + 1), obstaclePathFullRes=(sc.nObst, 2, T + 1),
+                  controlPathFullRes=(nV, T + 1), controlPredictions=(Hp, nV, Nsim),
+                  trajectoryPredictions=(Hp, 2, nV, Nsim), initial_pos=(1, 2, nV, Nsim),
+                  MPC_delay_compensation_trajectory=(10, 6, nV, Nsim),
+                  evaluations_obj_value=(1, 1), controllerRuntime=(Nsim, 1),
+                  stepTime=(Nsim, 1), ReferenceTrajectory=(Hp, 2, nV, Nsim))
+    assert set(back) == set(shapes)
+    for k, shp in shapes.items():
+        a = np.reshape(back[k], shp, order="F")
+        if k not in ("initial_pos", "evaluations_obj_value"):
+            assert np.array_equal(a, res[k], equal_nan=True), k
+    tps = sc.ticks_per_sim
+    veh = res["vehiclePathFullRes"]
+    assert np.all(np.isfinite(veh[:, :, :tps + 1])) and np.all(np.isnan(veh[:, :, tps + 1:]))
+    assert np.all(res["controlPredictions"][:, :, 1:] == 0)
+    assert np.allclose(res["obstaclePathFullRes"][:, :, 0], np.array(sc.obstacles)[:, 0:2])
