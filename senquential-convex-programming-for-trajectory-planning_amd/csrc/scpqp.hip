@@ -128,6 +128,9 @@ struct KArgs {
 // out-of-line functions take it by pointer without the copy to private memory
 // that taking the address of a by-value kernel parameter would force.
 typedef __attribute__((address_space(4))) const KArgs cKArgs;
+// the parameter block is written once before the launch: read it through the
+// constant address space so its fields come in as scalar loads
+typedef __attribute__((address_space(4))) const DevParams cParams;
 
 
 // ---------------------------------------------------------------------------
@@ -199,6 +202,7 @@ struct Lay {
     using HT = typename std::conditional<HG, gdouble, ldouble>::type;
     using VT = typename std::conditional<VG, gdouble, ldouble>::type;
     int V, O, Hb, N, n, m, mc, ld, mp, nb;
+    int lead;   // the wave that runs the serial parts (panel, triangular solves)
     ldouble *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
     ldouble *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr, *Wt;
     lint* rinfo;
@@ -210,6 +214,7 @@ template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
                                                     int O, int Hb) {
     Lay<HG, VG, RM, OCC> L;
+    L.lead = 0;
     L.V = V; L.O = O; L.Hb = Hb; L.N = V * Hb; L.n = L.N + 1;
     L.mp = V * (V - 1) / 2 * Hb;
     L.m = L.mp + V * O * Hb;
@@ -237,6 +242,11 @@ extern __shared__ double smem_[];   // dynamic LDS (one problem's state)
 // ---------------------------------------------------------------------------
 // Small helpers
 // ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long readfirstlane_u64(unsigned long long v) {
+    const unsigned lo = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v));
+    const unsigned hi = __builtin_amdgcn_readfirstlane(static_cast<unsigned>(v >> 32));
+    return (static_cast<unsigned long long>(hi) << 32) | lo;
+}
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     long long bits = __double_as_longlong(v);
     int lo = __builtin_amdgcn_readlane(static_cast<int>(bits & 0xffffffffll), lane);
@@ -400,9 +410,9 @@ __device__ double jac_entry(const ldouble* x, double u, double Lf, double Lr, do
 // Quirks B.1 (alternation past the end) and B.3 (rear-axle speed) reproduced;
 // B.2's float '^' (reference raises) is evaluated with '**' and flagged.
 // ---------------------------------------------------------------------------
-__device__ int sample_reference(const DevParams& P, int v, double vx, double vy, double step,
+__device__ int sample_reference(const cParams& P, int v, double vx, double vy, double step,
                                 int Hb, ldouble* out /* [Hb][2] */) {
-    const double* c = P.poly + v * P.maxPts * 2;
+    const auto* c = P.poly + v * P.maxPts * 2;
     const int np = P.npts[v];
     int flag = 0;
     // getShortestDistance: seeded with curve point 1, index 2 (quirk B.2)
@@ -598,7 +608,7 @@ __device__ void expm8(ldouble* scr, bool act, ldouble* red) {
 // (MPCclass, MPC_Iter.py:59-149), scaled cost gradient, row table.
 // ---------------------------------------------------------------------------
 template <class LT>
-__device__ int setup_problem(const cKArgs& a, const DevParams& P, const LT& L, int b) {
+__device__ int setup_problem(const cKArgs& a, const cParams& P, const LT& L, int b) {
     const int tid = threadIdx.x, V = L.V, O = L.O, Hb = L.Hb, Hm = P.hpMax;
     for (int i = tid; i < 6 * V; i += NT) L.x0[i] = a.x0[(size_t)b * V * 6 + i];
     for (int i = tid; i < V; i += NT) L.u0[i] = a.u0 ? a.u0[(size_t)b * V + i] : 0.0;
@@ -712,8 +722,13 @@ __device__ int setup_problem(const cKArgs& a, const DevParams& P, const LT& L, i
 // register allocation of the solve loop.
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int b, int Hb) {
+    // uniform arguments arrive in VGPRs: back to SGPRs (see uniform_ctx)
+    ap = (const cKArgs*)readfirstlane_u64((unsigned long long)ap);
+    ws = (gdouble*)readfirstlane_u64((unsigned long long)ws);
+    b = __builtin_amdgcn_readfirstlane(b);
+    Hb = __builtin_amdgcn_readfirstlane(Hb);
     const cKArgs& a = *ap;
-    const DevParams& P = *a.P;
+    const cParams& P = *(const cParams*)a.P;
     const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
     const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
@@ -842,7 +857,7 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
 // Normal matrix assembly  K = P_s + rho I + G' diag(d) G   (lower triangle)
 // ---------------------------------------------------------------------------
 template <class LT, class PD>
-__device__ void assemble(const DevParams& P, const LT& L, PD d, double rho) {
+__device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb;
     const double u2 = P.uLim * P.uLim;
     // phase 1: W~ blocks [k][a>=b] (2x2) and the omega-coupling vector in y-space (yb)
@@ -984,6 +999,14 @@ __device__ __forceinline__ double recip(double x) {
 __device__ __forceinline__ bool wave0() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x) < 64;   // wave-uniform branch
 }
+// The serial parts of a problem (panel factorisation, triangular solves) run on
+// one wave, the lead.  Each workgroup picks its lead on a different SIMD from
+// the other workgroups resident on its CU (lead_wave_elect), so their serial
+// chains do not share an issue port.
+__device__ __forceinline__ int wave_id() {
+    return __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
+}
+__device__ __forceinline__ bool is_lead(int lead) { return wave_id() == lead; }
 
 // Wave 0: factor the panel of columns [r0, r0 + jb) in registers, rows
 // i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB
@@ -1145,14 +1168,15 @@ __device__ bool cholesky(const LT& L) {
         const int jp = r0 - CB;   // previous panel (none at the first step)
         const int jb = min(CB, n - r0), r1 = r0 + jb;
         const ldouble* dprev = dbuf + (par ^ 1) * CB;
-        if (wave0()) {
+        if (is_lead(L.lead)) {
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
             ldouble* dn = dbuf + par * CB;
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
         } else if (jp >= 0 && r1 < n) {
-            trailing_update(L.H, n, jp, r1, dprev, (int)threadIdx.x - 64, NT - 64);
+            trailing_update(L.H, n, jp, r1, dprev,
+                            ((wave_id() - L.lead + 3) & 3) * 64 + (int)(threadIdx.x & 63), NT - 64);
         }
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
         unsigned long long _pb = __builtin_amdgcn_s_memtime();
@@ -1242,9 +1266,10 @@ struct Solver {
                     const int j = jc + q;
                     if (j < jend) {
                         const double xj = readlane_d(r[T], j & 63);
+                        r[T] -= cur[T][q] * xj;
                         xf[T] = (lane == (j & 63)) ? xj : xf[T];
 #pragma unroll
-                        for (int t = T; t < R; ++t) r[t] -= cur[t][q] * xj;
+                        for (int t = T + 1; t < R; ++t) r[t] -= cur[t][q] * xj;
                     }
                 }
                 shift();
@@ -1263,9 +1288,11 @@ struct Solver {
                     const int j = jc + q;
                     if (j < n) {
                         const double xj = readlane_d(r[T], j & 63);
+                        // the owner slot first: it carries the next step's broadcast
+                        r[T] -= cur[T][q] * xj;
                         xf[T] = (lane == (j & 63)) ? xj : xf[T];
 #pragma unroll
-                        for (int t = 0; t <= T; ++t) r[t] -= cur[t][q] * xj;
+                        for (int t = 0; t < T; ++t) r[t] -= cur[t][q] * xj;
                     }
                 }
                 shift();
@@ -1303,7 +1330,7 @@ __device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, l
 
 template <class LT>
 __device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
-    if (wave0()) {
+    if (is_lead(L.lead)) {
         const int n = L.n;
         constexpr int RM = LT::RMAX;
         if (RM == 1 || n <= 64) chol_solve_r<1>(L, bvec, x);
@@ -1325,7 +1352,7 @@ struct EvalRes {
 };
 
 template <class LT>
-__device__ EvalRes evaluate_u(const DevParams& P, const LT& L, const ldouble* u, double* cveh,
+__device__ EvalRes evaluate_u(const cParams& P, const LT& L, const ldouble* u, double* cveh,
                               double* cobs) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, O = L.O;
     toeplitz_apply(L, u, L.pb);
@@ -1388,7 +1415,7 @@ __device__ EvalRes evaluate_u(const DevParams& P, const LT& L, const ldouble* u,
 //   nrm = || [a_r uLim, -1] ||,  a_r = -2 d' calB_i,k (+ 2 d' calB_j,k)
 // ---------------------------------------------------------------------------
 template <class LT>
-__device__ void linearise_rows(const DevParams& P, const LT& L) {
+__device__ void linearise_rows(const cParams& P, const LT& L) {
     const int tid = threadIdx.x, Hb = L.Hb;
     toeplitz_apply(L, L.ub, L.ya);
     __syncthreads();
@@ -1459,7 +1486,7 @@ __device__ void g_apply(const LT& L, PX x, PO out, bool minus_h) {
 
 // residuals rd (n), rp (mc) at (z, s, lam); out = {max|rp|, max|rd|, gap, pobj}
 template <class LT>
-__device__ void residuals(const DevParams& P, const LT& L, double (&out)[4]) {
+__device__ void residuals(const cParams& P, const LT& L, double (&out)[4]) {
     const int tid = threadIdx.x, N = L.N, Hb = L.Hb;
     const double u2 = P.uLim * P.uLim;
     toeplitz_apply(L, L.z, L.ya);
@@ -1527,9 +1554,9 @@ __device__ double max_step(const LT& L) {
 // scalars live.  (One monolithic inlined body needed ~450 registers.)
 // ---------------------------------------------------------------------------
 struct Ctx {
-    const DevParams* P;
+    const cParams* P;
     gdouble* ws;
-    int Hb;
+    int Hb, lead;
 };
 struct D4 {
     double a, b, c, d;
@@ -1547,15 +1574,31 @@ __device__ __forceinline__ int polish_stop(const D4& d, int ref, double early) {
     return 0;
 }
 
+// Out-of-line phases receive Ctx in VGPRs (the calling convention passes every
+// argument per lane).  Its fields are workgroup-uniform: move them to SGPRs so
+// that the parameter loads are scalar and every size, loop bound and offset
+// derived from them stays scalar (SALU loop control, uniform branches).
+__device__ __forceinline__ Ctx uniform_ctx(const Ctx& c) {
+    Ctx u;
+    u.P = (const cParams*)readfirstlane_u64((unsigned long long)c.P);
+    u.ws = (gdouble*)readfirstlane_u64((unsigned long long)c.ws);
+    u.Hb = __builtin_amdgcn_readfirstlane(c.Hb);
+    u.lead = __builtin_amdgcn_readfirstlane(c.lead);
+    return u;
+}
+
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
     const Off f = plan_offsets(c.P->nV, c.P->nO, c.P->hpMax, HG, VG);
-    return make_lay<HG, VG, RM, OCC>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
+    Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
+    L.lead = c.lead;
+    return L;
 }
 #define PHASE template <bool HG, bool VG, int RM, int OCC> __device__ __noinline__
 #define LAYDEF                  \
-    const DevParams& P = *c.P;  \
-    const Lay<HG, VG, RM, OCC> L = lay_of<HG, VG, RM, OCC>(c); \
+    const Ctx cu_ = uniform_ctx(c); \
+    const cParams& P = *cu_.P;  \
+    const Lay<HG, VG, RM, OCC> L = lay_of<HG, VG, RM, OCC>(cu_); \
     (void)P
 #define PH(f) f<HG, VG, RM, OCC>
 
@@ -1588,7 +1631,7 @@ PHASE D4 ph_residuals(Ctx c) {
 }
 // rhs = -q + G'(tv) with tv = h (init) or tv = mask (h/delta - y) (polish), + rho x_k
 template <class LT>
-__device__ __forceinline__ void rhs_from_tv_body(const DevParams& P, const LT& L, double rho) {
+__device__ __forceinline__ void rhs_from_tv_body(const cParams& P, const LT& L, double rho) {
     const double ow = gt_apply(L, L.tv, L.rhs);
     if (threadIdx.x == 0) L.rhs[L.N] = ow - P.slackW + rho * L.dz[L.N];
     __syncthreads();
@@ -1754,7 +1797,7 @@ PHASE D4 ph_scales(Ctx c) {
 }
 // polish right-hand side: tv = mask (h / delta - y), rhs = -q + G' tv + rho x_k
 template <class LT>
-__device__ __forceinline__ void polish_rhs_body(const DevParams& P, const LT& L) {
+__device__ __forceinline__ void polish_rhs_body(const cParams& P, const LT& L) {
     const double idl = 1.0 / P.polDelta;
     for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
     __syncthreads();
@@ -1768,7 +1811,7 @@ PHASE void ph_polish_rhs(Ctx c) {
 // {max |x_k - x_{k-1}|, max |x_k|, max rp over the inactive rows, -min y over
 // the active rows} (x_{k-1} kept in rd, dead during the polish).
 template <class LT>
-__device__ __forceinline__ D4 polish_dual_body(const DevParams& P, const LT& L) {
+__device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
     const double idl = 1.0 / P.polDelta;
     g_apply(L, L.dz, L.rp, true);
     double viol = -1e300, yneg = -1e300;
@@ -1878,15 +1921,14 @@ struct QpStats {
 // P.nRefine solves per round), certified, else the active set is corrected
 // (primal-dual active set) and the round repeats.  Returns true if certified.
 template <bool HG, bool VG, int RM, int OCC>
-__device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds, int cap,
-                                              double early, QpStats& st) {
-    const DevParams& P = *c.P;
+__device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, int max_rounds,
+                                              int cap, double early, QpStats& st) {
     bool ok = false, refactor = true, extended = false;
     PROF_T0();
     for (int round = 0; round < max_rounds && !ok; ++round) {
         ++st.rounds;
         if (refactor) {
-            PH(ph_assemble)(c, P.polRho);
+            PH(ph_assemble)(c, rho);
             const bool fact = PH(ph_cholesky)(c) != 0;
             PROF_ACC(7);
             if (!fact) break;
@@ -1917,15 +1959,24 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, int max_rounds
 // One convexified QP.  warm: try the previous QP's active set first (a few
 // polish rounds, no interior point iterations); on failure, or cold, run the
 // Mehrotra IPM from the CVXOPT initial point and polish its active set.
+// The driver keeps its counters and the parameters its loops test in
+// registers: the callers' QpStats/flags live on the private stack, and a
+// parameter re-read after every out-of-line phase is a global-memory load on
+// the iteration's critical path.
+struct QpKnobs {
+    int maxIpm, nRefine, mc;
+    double ipmTol, polRho;
+};
 template <bool HG, bool VG, int RM, int OCC>
-__device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st) {
-    const DevParams& P = *c.P;
-    const int mc = (P.nV * (P.nV - 1) / 2 + P.nV * P.nO) * c.Hb + 2 * P.nV * c.Hb + 1;
+__device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qflags, bool warm,
+                                              QpStats& st) {
+    const int mc = K.mc;
     const D4 sc = PH(ph_scales)(c);
     const double hmax = sc.a, qmax = sc.b;
     if (warm) {
         PH(ph_polish_warm)(c);
-        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, kWarmRounds, kWarmRefine, kWarmEarly, st)) {
+        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, kWarmRounds, kWarmRefine, kWarmEarly,
+                                           st)) {
             ++st.warm_ok;
             return true;
         }
@@ -1944,10 +1995,10 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
     bool conv = false;
     D4 res = PH(ph_residuals)(c);
     PROF_ACC(1);
-    for (; it < P.maxIpm; ++it) {
+    for (; it < K.maxIpm; ++it) {
         PROF_ACC(0);
-        if (res.a <= P.ipmTol * hmax && res.b <= P.ipmTol * qmax &&
-            res.c <= P.ipmTol * fmax(1.0, fabs(res.d))) {
+        if (res.a <= K.ipmTol * hmax && res.b <= K.ipmTol * qmax &&
+            res.c <= K.ipmTol * fmax(1.0, fabs(res.d))) {
             conv = true;
             break;
         }
@@ -1966,21 +2017,67 @@ __device__ __noinline__ bool qp_solve(Ctx c, int* qflags, bool warm, QpStats& st
         PROF_ACC(6);
     }
     st.ipm += it;
-    if (!conv && it >= P.maxIpm) *qflags |= SCPQP_FL_IPM_MAXIT;
+    if (!conv && it >= K.maxIpm) qflags |= SCPQP_FL_IPM_MAXIT;
     // ---- active-set polish on {lam > s}
     PH(ph_polish_prep)(c);
-    const bool ok = polish_rounds<HG, VG, RM, OCC>(c, hmax, kPolishRounds, P.nRefine, INFINITY, st);
-    if (!ok) *qflags |= SCPQP_FL_POLISH_REJECTED;
+    const bool ok = polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, kPolishRounds, K.nRefine,
+                                                   INFINITY, st);
+    if (!ok) qflags |= SCPQP_FL_POLISH_REJECTED;
+    return ok;
+}
+template <bool HG, bool VG, int RM, int OCC>
+__device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, QpStats& st) {
+    const Ctx c = uniform_ctx(c0);
+    const cParams& P = *c.P;
+    QpKnobs K;
+    K.maxIpm = __builtin_amdgcn_readfirstlane(P.maxIpm);
+    K.nRefine = __builtin_amdgcn_readfirstlane(P.nRefine);
+    K.mc = __builtin_amdgcn_readfirstlane(
+        (P.nV * (P.nV - 1) / 2 + P.nV * P.nO) * c.Hb + 2 * P.nV * c.Hb + 1);
+    K.ipmTol = P.ipmTol;
+    K.polRho = P.polRho;
+    QpStats ls{0, 0, 0, 0};
+    int lf = 0;
+    const bool ok = qp_solve_body<HG, VG, RM, OCC>(c, K, lf, warm, ls);
+    st.ipm += ls.ipm;
+    st.rounds += ls.rounds;
+    st.refine += ls.refine;
+    st.warm_ok += ls.warm_ok;
+    *qflags |= lf;
     return ok;
 }
 
 // ---------------------------------------------------------------------------
 // Kernel
 // ---------------------------------------------------------------------------
+// Lead election: one counter per CU (XCC, SE, SH, CU from the hardware
+// registers); the k-th workgroup of a launch on a CU takes the wave that sits on
+// SIMD k mod 4.  The persistent workgroups stay resident for the whole launch,
+// and the counters only ever grow, so consecutive launches keep handing out
+// consecutive SIMDs.  A placement heuristic only: any lead is correct.
+__device__ unsigned g_cu_ctr[4096];
+__device__ __forceinline__ int lead_wave_elect(lint* sh) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20);   // HW_REG_XCC_ID [3:0]
+    const int simd = (hw >> 4) & 3;
+    if (threadIdx.x == 0) {
+        const unsigned key = ((xcc & 15) << 8) | (((hw >> 13) & 7) << 5) | (((hw >> 12) & 1) << 4) |
+                             ((hw >> 8) & 15);
+        sh[0] = atomicAdd(&g_cu_ctr[key], 1u) & 3;
+        sh[1] = 0;
+    }
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0 && simd == sh[0]) sh[1] = threadIdx.x >> 6;
+    __syncthreads();
+    const int lead = __builtin_amdgcn_readfirstlane(sh[1]);
+    __syncthreads();
+    return lead;
+}
+
 template <bool HG, bool VG, int RM, int OCC>
 __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     ldouble* smem = (ldouble*)smem_;
-    const DevParams& P = *a.P;
+    const cParams& P = *(const cParams*)a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
     const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
@@ -1991,6 +2088,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     ldouble* lg = smem + f.g;
     ldouble* lp0 = smem + f.p0;
     ldouble* lqs = smem + f.qs;
+    const int lead = lead_wave_elect((lint*)(smem + f.red + 126));
     for (;;) {
         if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
         __syncthreads();
@@ -2012,7 +2110,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             __syncthreads();
             continue;
         }
-        const Ctx c{a.P, ws, Hb};
+        const Ctx c{(const cParams*)a.P, ws, Hb, lead};
         const int V = P.nV, N = V * Hb, O = P.nO;
 #ifdef SCPQP_PROF
         if (tid == 0 && b < 8192) g_ptime[2 * b] = __builtin_amdgcn_s_memrealtime();
