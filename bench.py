@@ -177,6 +177,26 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)   # one launch per step
     elapsed = shard.max_over_ranks(elapsed, dist, dev)
 
+    # end-to-end leg: host (pinned) inputs -> H2D -> solve -> D2H of the result
+    # arrays main.py consumes (u, traj, status, obj, max_violation); reported beside `value`,
+    # never as it
+    h_in = [t.cpu().pin_memory() for t in (x0, u0, ec)]
+    d_in = [torch.empty_like(t) for t in (x0, u0, ec)]
+    outs = (out.u, out.traj, out.status, out.obj, out.max_violation)
+    h_out = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in outs]
+    e2e_steps = max(min(args.steps, 5), 1)
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    for _ in range(e2e_steps):
+        for d, h in zip(d_in, h_in):
+            d.copy_(h, non_blocking=True)
+        S.solve(d_in[0], d_in[1], d_in[2], hp=hpt, out=out)
+        for h, d in zip(h_out, outs):
+            h.copy_(d, non_blocking=True)
+        torch.cuda.synchronize()
+    e2e_s = shard.max_over_ranks(time.perf_counter() - te, dist, dev)
+    e2e_value = world * B * e2e_steps / e2e_s
+
     n_scp = out.n_scp.cpu().numpy()
     n_ipm = out.n_ipm.cpu().numpy()
     status = out.status.cpu().numpy()
@@ -232,6 +252,9 @@ def main():
         "warm_certified_qp_frac": float(n_warm.sum() / max(n_scp.sum(), 1)),
         "mean_polish_solves_per_qp": float(n_ref.sum() / max(n_scp.sum(), 1)),
         "status_converged_frac": float(np.mean((status & 0xff) == 0)),
+        "e2e_solves_per_s": e2e_value,
+        "e2e_note": f"host pinned inputs, H2D + solve + D2H of u/traj/status/obj/max_violation, "
+                    f"synchronised per step, {e2e_steps} steps",
     }
     if cpu is not None:
         trajs = out.traj.cpu().numpy()
