@@ -2305,6 +2305,15 @@ int plan(scpqp_handle* h) {
     h->wsStride = f.ws;
     h->grid = h->cus * bestPer;
     h->occ = bestPer >= 3 ? 3 : 2;
+#ifdef SCPQP_OCC4
+    // diagnostic build: 4 workgroups per CU on plan 2 (matrix and vectors in the
+    // workspace), register budget compiled for 4 (128 VGPRs)
+    if (getenv("SCPQP_OCC4") && best == 2 && kLdsLimit / h->ldsBytes >= 4 &&
+        (V * Hm + 1 + 63) / 64 == 2) {
+        h->grid = h->cus * 4;
+        h->occ = 4;
+    }
+#endif
     return 0;
 }
 
@@ -2338,6 +2347,9 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
     const int occ = h->occ;   // workgroups per CU the register budget is compiled for
+#ifdef SCPQP_OCC4
+    if (occ == 4) return launch_t<true, true, 2, 4>(h, a, st, grid);
+#endif
 #define SCPQP_DISPATCH(HGV, VGV)                                              \
     switch (R * 4 + occ) {                                                   \
         case 6: return launch_t<HGV, VGV, 1, 2>(h, a, st, grid);             \
