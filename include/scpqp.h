@@ -122,6 +122,22 @@ typedef struct scpqp_batch_out {
     int32_t* n_polish;       /* [B] active-set polish rounds summed over the QPs       */
     int32_t* n_refine;       /* [B] multiplier-iteration solves summed over the QPs    */
     int32_t* n_warm;         /* [B] QPs certified from the previous QP's active set    */
+    double* trace;           /* [B][trace_iters][trace_stride] per-SCP-iteration record
+                                (SCP_controller.py:169-189 optimization_log), or NULL.
+                                Layout of one iteration (doubles), see scpqp_trace_layout:
+                                  [0] delta  [1] obj  [2] max_violation  [3] sum_violations
+                                  [4] slack omega = z[N]  [5] IPM iterations of this QP
+                                  [6] QP flags (1 certified, 2 warm-started)  [7] feasible
+                                  [8, 8+N)        u_lin: the iterate the rows linearise at
+                                  [8+N, 8+2N)     u: this QP's solution z[:N]
+                                  [8+2N, 8+2N+4m) rows r: e_r[0], e_r[1], w_r, h_r (scaled
+                                                  factored row); Aineq/bineq
+                                                  follow as A_r = -(e_r.g) nrm/uLim,
+                                                  b_r = h_r nrm, nrm = -1/w_r
+                                N = n_veh*hp_max, m = pair + obstacle rows at hp_max;
+                                a problem of horizon hp_b fills the prefixes of each part
+                                (N_b = n_veh*hp_b, m_b rows).  Iterations past
+                                trace_iters are not recorded.                          */
 } scpqp_batch_out;
 
 /* outputs of scpqp_linearize (MPCclass intermediates; DEVICE pointers, any may be NULL) */
@@ -178,6 +194,10 @@ int scpqp_sample_reference(scpqp_handle* h, int32_t B, const scpqp_batch_in* in,
  * uses for this handle (diagnostics / roofline bookkeeping). */
 int scpqp_resources(scpqp_handle* h, int64_t* lds_bytes, int64_t* ws_bytes_per_wg,
                     int32_t* big_mode, int32_t* grid);
+
+/* Shape of scpqp_batch_out.trace for this handle: doubles per iteration and
+ * iterations per problem (= the handle's max_scp_iter). */
+int scpqp_trace_layout(scpqp_handle* h, int32_t* stride_doubles, int32_t* iters);
 
 /* ------------------------------------------------------------------------
  * The bicycle plant around the solve (csrc/plant.hip).  Handle-free; every

@@ -13,9 +13,12 @@ What differs from the reference, on purpose:
 * the QP backend is the kernel's interior point method + active-set polish
   instead of cvxpy/GUROBI (the QP is strictly convex, so the minimiser is the
   same to solver tolerance; see DESIGN.md);
-* ``optimization_log`` holds per-solve counters (SCP iterations, IPM
-  iterations, status flags) instead of the dense per-iteration tensors, which
-  main.py never reads;
+* ``optimization_log`` holds the reference's per-iteration lists
+  (SCP_controller.py:169-189: 'Aineq', 'bineq', 'x', 'slack', 'QCQP_ObjVal',
+  'SCP_ObjVal', 'delta', 'u', 'prev_u', 'feasible'), rebuilt from the kernel's
+  per-iteration trace, plus per-solve counters (SCP/IPM iterations, status
+  flags).  'P', 'q', 'lb', 'ub' are the same every iteration and are not
+  repeated; the forward_U trajectories of the log are not rebuilt;
 * the dense ``qcqp`` dictionary (QCQP_formulate, SCP_controller.py:278-341) is
   built lazily, only if a caller reads ``.qcqp``; the solve uses the
   factored forms on the device.
@@ -86,7 +89,8 @@ class SCPcontroller:
         Returns (u, feasible, objective, log)."""
         if abs(u_approx[0, 0]) < np.spacing(1):     # in place, like the reference (:75-76)
             u_approx[0] = np.spacing(1)
-        res = self.solver.solve(u_warm=np.asarray(u_approx, float).reshape(1, -1), **self._inputs())
+        res = self.solver.solve(u_warm=np.asarray(u_approx, float).reshape(1, -1), trace=True,
+                                **self._inputs())
         u = res.u[0, :self.nVeh * self.Hp].cpu().numpy().reshape(-1, 1)
         status = int(res.status[0].item())
         log = {'status': status & 0xff, 'flags': status & ~0xff,
@@ -94,8 +98,45 @@ class SCPcontroller:
                'obj': float(res.obj[0].item()),
                'max_violation': float(res.max_violation[0].item()),
                'sum_violations': float(res.sum_violations[0].item())}
+        log.update(self._iteration_log(res))
         self._last_traj = res.traj[0, :self.Hp].cpu().numpy()
         return u, bool(res.feasible[0].item()), float(res.obj[0].item()), log
+
+    def _iteration_log(self, res):
+        """The reference's per-iteration optimization_log lists (SCP_controller.py:169-189)
+        from the device trace: dense Aineq/bineq from the factored rows and the
+        Toeplitz blocks, x = [u; slack], SCP_ObjVal = 1/2 x'Px + q'x + gamma0."""
+        from scpqp import trace as TR
+        nV, Hp, nO = self.nVeh, self.Hp, self.nObst
+        m = self.mpc
+        g = np.stack([m.Mathcal_B[0::2, 0, v] for v in range(nV)], 0)        # g_k x-components
+        g = np.stack([g, np.stack([m.Mathcal_B[1::2, 0, v] for v in range(nV)], 0)], -1)
+        its = TR.decode(res.trace[0].cpu().numpy(), int(res.n_scp[0].item()), nV, nO, Hp,
+                        self.solver.hp_max, g=g, u_lim=self.scenario_uLim)
+        Phi0 = np.zeros((nV * Hp, nV * Hp))
+        Psi0 = np.zeros(nV * Hp)
+        for v in range(nV):
+            sl = slice(v * Hp, (v + 1) * Hp)
+            Phi0[sl, sl] = m.Phi_0[:, :, v]
+            Psi0[sl] = m.Psi_0[:, 0, v]
+        gamma0 = float(np.sum(m.gamma_0))
+        log = {k: [] for k in ('Aineq', 'bineq', 'x', 'slack', 'SCP_ObjVal', 'QCQP_ObjVal',
+                               'delta', 'u', 'feasible', 'prev_u', 'ipm_iters')}
+        for d in its:
+            uu = d['z'][:-1]
+            log['Aineq'].append(d['A'])
+            log['bineq'].append(d['b'].reshape(-1, 1))
+            log['x'].append(d['z'].reshape(-1, 1))
+            log['slack'].append(d['slack'])
+            log['SCP_ObjVal'].append(float(uu @ Phi0 @ uu + Psi0 @ uu + 1e5 * d['slack'] + gamma0))
+            log['QCQP_ObjVal'].append(np.array([[d['obj']]]))
+            log['delta'].append(d['delta'])
+            log['u'].append(uu.reshape(-1, 1))
+            log['feasible'].append(d['feasible'])
+            log['prev_u'].append(d['u_lin'].reshape(-1, 1))
+            log['ipm_iters'].append(d['ipm_iters'])
+        log['trace'] = its          # decoded kernel records (max_violation per iteration, rows)
+        return log
 
     # ------------------------------------------------------------------ SCP_controller.py:199-213
     def forward_U(self, u):

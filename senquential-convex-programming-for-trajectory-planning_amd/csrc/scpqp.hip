@@ -120,6 +120,7 @@ struct KArgs {
     int *status, *nscp, *nipm, *feas, *npol, *nref, *nwarm;
     double *Ad, *Bd, *Ed, *gOut, *p0Out, *psiOut, *refOut;
     double *cveh, *cobs;
+    double* trace;
     double* ws;
     long long wsStride;
     int* counter;
@@ -141,6 +142,12 @@ typedef __attribute__((address_space(4))) const DevParams cParams;
 // indexing uses the problem's own horizon, so mixed horizons share a launch.
 // ---------------------------------------------------------------------------
 __host__ __device__ inline int pad2(int x) { return (x + 1) & ~1; }
+
+// doubles per SCP iteration of the optional trace (scpqp.h, scpqp_batch_out.trace)
+__host__ __device__ inline int trace_stride(int V, int O, int Hm) {
+    const int N = V * Hm, m = V * (V - 1) / 2 * Hm + V * O * Hm;
+    return pad2(8 + 2 * N + 4 * m);
+}
 
 // Packed lower-triangular storage of the KKT matrix: row i holds columns 0..i,
 // padded to an even length so every row starts 16-byte aligned.
@@ -1896,6 +1903,35 @@ PHASE void ph_take_u(Ctx c) {
     __syncthreads();
 }
 
+// Per-iteration trace (scpqp_batch_out.trace), written only when requested.
+// Before take_u: the linearisation point u-bar and the factored rows it gave.
+PHASE void ph_trace_rows(Ctx c, double* dst) {
+    LAYDEF;
+    for (int i = threadIdx.x; i < L.N; i += NT) dst[8 + i] = L.ub[i];
+    const int N2 = 8 + 2 * P.nV * P.hpMax;
+    for (int r = threadIdx.x; r < L.m; r += NT) {
+        dst[N2 + 4 * r] = L.rowE[2 * r];
+        dst[N2 + 4 * r + 1] = L.rowE[2 * r + 1];
+        dst[N2 + 4 * r + 2] = L.rowW[r];
+        dst[N2 + 4 * r + 3] = L.rowH[r];
+    }
+}
+// After the evaluation: the QP's solution, its slack and the stopping-rule terms.
+PHASE void ph_trace_sol(Ctx c, double* dst, D4 ev, double delta, int ipm, int qfl) {
+    LAYDEF;
+    for (int i = threadIdx.x; i < L.N; i += NT) dst[8 + P.nV * P.hpMax + i] = L.ub[i];
+    if (threadIdx.x == 0) {
+        dst[0] = delta;
+        dst[1] = ev.a;
+        dst[2] = ev.b;
+        dst[3] = ev.c;
+        dst[4] = L.z[L.N];
+        dst[5] = ipm;
+        dst[6] = qfl;
+        dst[7] = ev.d;
+    }
+}
+
 // Active-set corrections of the polish (oracle POLISH_ROUNDS), the rounds a
 // warm start may take before the IPM runs, and the multiplier iteration's
 // convergence test (oracle POLISH_TOL).
@@ -2177,6 +2213,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
         int qflags = 0, it = 0, status = SCPQP_ST_MAX_SCP;
         QpStats qs{0, 0, 0, 0};
         const bool warm_on = (P.flags & SCPQP_FLAG_COLD_QP) == 0;
+        const int trStride = trace_stride(V, O, P.hpMax);
         bool prev_ok = false;   // previous QP certified: its active set seeds the next one
         for (it = 0; it < maxScp; ++it) {
 #ifdef SCPQP_PROF
@@ -2187,14 +2224,22 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             // warm start from the previous QP's active set from the third QP on: the
             // first re-linearisation moves the active set too far for a few
             // active-set corrections to recover it (tools/polish_study.py: 0/16)
-            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_on && prev_ok && it >= 2, qs);
+            const int ipm_before = qs.ipm;
+            const bool warm_qp = warm_on && prev_ok && it >= 2;
+            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_qp, qs);
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
+            double* trp = (a.trace && it < P.maxScp) ? a.trace + ((size_t)b * P.maxScp + it) * trStride
+                                                     : nullptr;
+            if (trp) PH(ph_trace_rows)(c, trp);
             PH(ph_take_u)(c);
             ev = PH(ph_evaluate)(c, nullptr, nullptr);
             PROF_ACC(17);
             const double delta = (obj0 + P.slackW * mv0) - (ev.obj + P.slackW * ev.maxv);
+            if (trp)
+                PH(ph_trace_sol)(c, trp, D4{ev.obj, ev.maxv, ev.sumv, (double)ev.feasible}, delta,
+                                 qs.ipm - ipm_before, (prev_ok ? 1 : 0) | (warm_qp ? 2 : 0));
             obj0 = ev.obj;
             mv0 = ev.maxv;
             if (!isfinite(ev.obj)) {
@@ -2404,7 +2449,7 @@ extern "C" {
 
 const char* scpqp_last_error(void) { return g_err; }
 
-const char* scpqp_version(void) { return "scpqp-mi355x 0.3 (gfx950, fp64)"; }
+const char* scpqp_version(void) { return "scpqp-mi355x 0.4 (gfx950, fp64)"; }
 
 int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpqp_handle** out) {
     if (!dims || !p || !out) return fail(SCPQP_E_ARG, "null argument%s");
@@ -2510,6 +2555,7 @@ int scpqp_solve(scpqp_handle* h, int32_t B, const scpqp_batch_in* in, const scpq
     a.npol = out->n_polish;
     a.nref = out->n_refine;
     a.nwarm = out->n_warm;
+    a.trace = out->trace;
     return launch(h, a, static_cast<hipStream_t>(stream));
 }
 
@@ -2576,6 +2622,13 @@ int scpqp_prof_read(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+
+int scpqp_trace_layout(scpqp_handle* h, int32_t* stride, int32_t* iters) {
+    if (!h) return fail(SCPQP_E_ARG, "null handle%s");
+    if (stride) *stride = trace_stride(h->dims.n_veh, h->dims.n_obst, h->dims.hp_max);
+    if (iters) *iters = h->hostP.maxScp;
+    return 0;
+}
 
 int scpqp_resources(scpqp_handle* h, int64_t* lds, int64_t* ws, int32_t* big, int32_t* grid) {
     if (!h) return fail(SCPQP_E_ARG, "null handle%s");

@@ -58,7 +58,7 @@ class BatchOut(C.Structure):
                 ("n_scp", C.c_void_p), ("n_ipm", C.c_void_p), ("obj", C.c_void_p),
                 ("max_violation", C.c_void_p), ("sum_violations", C.c_void_p),
                 ("feasible", C.c_void_p), ("n_polish", C.c_void_p), ("n_refine", C.c_void_p),
-                ("n_warm", C.c_void_p)]
+                ("n_warm", C.c_void_p), ("trace", C.c_void_p)]
 
 
 class LinOut(C.Structure):
@@ -80,6 +80,7 @@ class PlantParams(C.Structure):
 # every symbol include/scpqp.h declares (checked by tests/test_abi.py)
 EXPORTS = ("scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version", "scpqp_solve",
            "scpqp_linearize", "scpqp_evaluate", "scpqp_sample_reference", "scpqp_resources",
+           "scpqp_trace_layout",
            "scpqp_delay_compensate", "scpqp_plant_step", "scpqp_clip_controls")
 
 _lib = None
@@ -115,6 +116,8 @@ def load(path=None):
     lib.scpqp_resources.argtypes = [H, C.POINTER(C.c_int64), C.POINTER(C.c_int64),
                                     C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
     lib.scpqp_resources.restype = C.c_int
+    lib.scpqp_trace_layout.argtypes = [H, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
+    lib.scpqp_trace_layout.restype = C.c_int
     PP = C.POINTER(PlantParams)
     V = C.c_void_p
     lib.scpqp_delay_compensate.argtypes = [PP, C.c_int32, C.c_double, C.c_int32, V, V, V, V, V,

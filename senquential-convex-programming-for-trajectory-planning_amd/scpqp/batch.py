@@ -119,3 +119,24 @@ def make_batch(scenario, B, base_seed=0, offset=0, perturb=True, noise=True, hp=
             base = obstacle_prediction(scenario, int(H)).reshape(-1)
             flat[hps == H, :base.size] = base
     return Batch(np.ascontiguousarray(x0), u0, ec, hps, obst, hp_max, seeds)
+
+
+def pack_slots(natural, hp, trailing_hp_axis):
+    """Natural per-problem arrays -> the packed per-slot layout the C-ABI reads.
+
+    ``natural`` is [B, ..., hp_max] with the horizon on axis ``trailing_hp_axis``
+    (counted within one problem: obst [nObst, 2, hp_max] -> axis 2, ref_points
+    [hp_max, 2, nVeh] -> axis 0, u_warm [nVeh, hp_max] -> axis 1).  Problem b's
+    slot receives its first hp[b] steps as one contiguous prefix, i.e. the
+    array [..., hp_b] C-contiguous, zero-padded to the slot size.  For hp_b ==
+    hp_max this is the identity."""
+    nat = np.asarray(natural, float)
+    B = nat.shape[0]
+    out = np.zeros((B, int(np.prod(nat.shape[1:]))))
+    for b in range(B):
+        H = int(hp[b])
+        sl = [slice(None)] * (nat.ndim - 1)
+        sl[trailing_hp_axis] = slice(0, H)
+        blk = np.ascontiguousarray(nat[b][tuple(sl)]).reshape(-1)
+        out[b, :blk.size] = blk
+    return out.reshape(nat.shape)

@@ -88,7 +88,7 @@ def held_command_tick(tick_now, tdx, tdu, tps, ticks_total):
 
 class ClosedLoopBatch:
     def __init__(self, scenario, B, device=None, h_max=PL.H_MAX, keep_path=False, evaluate=True,
-                 timing=False, **solver_kw):
+                 timing=False, trace=False, **solver_kw):
         self.sc = scenario
         self.B = int(B)
         self.device = torch.device(device or "cuda")
@@ -114,7 +114,8 @@ class ClosedLoopBatch:
         self.state = torch.zeros((self.B, self.nV, 6), **f)
         self.last_path = None          # [B, nV, tps + 1, 6] of the previous step
         self.u_prev = None
-        self.out = self.solver.alloc_out(self.B)
+        self.trace = trace      # keep every step's solve inputs and per-SCP-iteration trace
+        self.out = self.solver.alloc_out(self.B, trace=trace)
         self.history = []
 
     def reset(self, x_init, noise=None):
@@ -180,7 +181,8 @@ class ClosedLoopBatch:
                                         noise=self.noise, h_max=self.h_max, device=self.device)
         # SCP solve, warm-started from the previous controller output (SCP_controller.py:42-43)
         obst = self._obstacle_prediction(max(0, tick_now - self.tdx))
-        out = self.solver.solve(x0, u_hold, u_warm=self.u_prev, obst=obst, out=self.out)
+        u_warm = self.u_prev
+        out = self.solver.solve(x0, u_hold, u_warm=u_warm, obst=obst, out=self.out)
         self.u_prev = out.u.clone()
         if self.timing:
             torch.cuda.synchronize(self.device)
@@ -212,6 +214,13 @@ class ClosedLoopBatch:
         if self.keep_path:
             rec["path"] = path
             rec["delay_traj"] = dtraj
+            rec["u_tick"] = u_tick
+            rec["x_start"] = path[:, :, 0, :]
+        if self.trace:
+            rec["u_warm"] = u_warm
+            rec["obst"] = obst
+            rec["trace"] = out.trace.clone()
+            rec["u"] = out.u.clone()
         if self.timing:
             torch.cuda.synchronize(self.device)
         rec["controllerRuntime"] = t_ctrl               # batch latency: every realisation

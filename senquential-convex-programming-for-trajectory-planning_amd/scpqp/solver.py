@@ -51,6 +51,7 @@ class SolveResult:
     n_polish: torch.Tensor   # active-set polish rounds (all QPs of the problem)
     n_refine: torch.Tensor   # multiplier-iteration solves (all QPs)
     n_warm: torch.Tensor     # QPs certified from the previous QP's active set
+    trace: torch.Tensor = None   # [B, trace_iters, trace_stride] per-SCP-iteration record, or None
 
 
 class ScpQpSolver:
@@ -64,6 +65,8 @@ class ScpQpSolver:
         self.lib = LB.load()
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
             else torch.device(device)
+        if self.device.index is None:          # "cuda" -> the current device, explicitly
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.nV = int(scenario.nVeh)
         self.nO = int(scenario.nObst)
         self.hp_max = int(hp_max or scenario.Hp)
@@ -140,20 +143,33 @@ class ScpQpSolver:
 
     def _inputs(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None,
                 u_warm=None, max_scp_iter=0, need_obst=True):
+        """Move the inputs to the device and check every size against (B, nVeh, nObst,
+        hp_max) before anything is launched: the kernel indexes each per-problem slot
+        with hp_max strides.  Per-problem slots are sized for hp_max; a problem of
+        horizon hp_b reads the PACKED prefix of its slot (obst [nObst][2][hp_b],
+        ref_points [hp_b][2][nVeh], u_warm [nVeh*hp_b]), which equals the natural
+        layout whenever hp_b == hp_max (scpqp.batch.pack_slots packs natural arrays)."""
         x0 = self._dev(x0)
-        B = x0.shape[0]
+        B = x0.shape[0] if x0.dim() > 0 else 0
         if B > self.max_batch:
             raise ValueError("batch larger than max_batch")
-        nV, Hm = self.nV, self.hp_max
+        nV, nO, Hm = self.nV, self.nO, self.hp_max
+        _need(x0, B * nV * 6, "x0 [B, nVeh, 6]")
         u0 = self._dev(u0) if u0 is not None else torch.zeros(B, nV, dtype=torch.float64,
                                                              device=self.device)
+        _need(u0, B * nV, "u0 [B, nVeh]")
         ec = self._dev(ec_noise)
+        _need(ec, B * nV * 2, "ec_noise [B, nVeh, 2]")
         hpt = self._dev(hp, torch.int32)
-        if need_obst and self.nO and obst is None:
+        _need(hpt, B, "hp [B]")
+        if need_obst and nO and obst is None:
             raise ValueError("scenario has obstacles: pass obst [B, nObst, 2, Hp]")
-        ob = self._dev(obst)
+        ob = self._dev(obst) if nO else None
+        _need(ob, B * nO * 2 * Hm, "obst [B, nObst, 2, hp_max] (packed per slot)")
         rp = self._dev(ref_points)
+        _need(rp, B * Hm * 2 * nV, "ref_points [B, hp_max, 2, nVeh] (packed per slot)")
         uw = self._dev(u_warm)
+        _need(uw, B * nV * Hm, "u_warm [B, nVeh*hp_max] (packed per slot)")
         bufs = (x0, u0, ec, hpt, ob, rp, uw)
         bi = LB.BatchIn(x0=_vptr(x0), u0=_vptr(u0), ec_noise=_vptr(ec), hp=_vptr(hpt),
                         obst=_vptr(ob), ref_points=_vptr(rp), u_warm=_vptr(uw),
@@ -165,33 +181,68 @@ class ScpQpSolver:
 
     # ------------------------------------------------------------------ entry points
     def solve(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None, u_warm=None,
-              max_scp_iter=0, out=None):
+              max_scp_iter=0, out=None, trace=False):
         """SCP_controller for a batch.  Arrays: x0 [B,nVeh,6], u0 [B,nVeh], ec_noise [B,nVeh,2],
-        hp [B] int, obst [B,nObst,2,Hp], ref_points [B,Hp,2,nVeh], u_warm [B,nVeh*Hp]."""
+        hp [B] int, obst [B,nObst,2,hp_max], ref_points [B,hp_max,2,nVeh], u_warm
+        [B,nVeh*hp_max]; per-problem slots are read as packed prefixes for hp_b < hp_max
+        (see _inputs).  ``trace=True`` also records every SCP iteration (the reference's
+        optimization_log, SCP_controller.py:169-189) into ``out.trace``; decode it with
+        scpqp.trace.decode."""
         B, bi, bufs = self._inputs(x0, u0, ec_noise, hp, obst, ref_points, u_warm, max_scp_iter)
         if out is None:
-            out = self.alloc_out(B)
+            out = self.alloc_out(B, trace=trace)
+        self._check_out(out, B)
         bo = LB.BatchOut(u=_vptr(out.u), traj=_vptr(out.traj), status=_vptr(out.status),
                          n_scp=_vptr(out.n_scp), n_ipm=_vptr(out.n_ipm), obj=_vptr(out.obj),
                          max_violation=_vptr(out.max_violation),
                          sum_violations=_vptr(out.sum_violations), feasible=_vptr(out.feasible),
                          n_polish=_vptr(out.n_polish), n_refine=_vptr(out.n_refine),
-                         n_warm=_vptr(out.n_warm))
+                         n_warm=_vptr(out.n_warm), trace=_vptr(out.trace))
         LB.check(self.lib.scpqp_solve(self.h, B, C.byref(bi), C.byref(bo), self._stream()),
                  self.lib)
         self._last_inputs = bufs   # keep device inputs alive until the stream consumes them
         return out
 
-    def alloc_out(self, B):
+    def trace_layout(self):
+        """(doubles per SCP iteration, iterations per problem) of SolveResult.trace."""
+        st, it = C.c_int32(), C.c_int32()
+        LB.check(self.lib.scpqp_trace_layout(self.h, C.byref(st), C.byref(it)), self.lib)
+        return st.value, it.value
+
+    def alloc_out(self, B, trace=False):
         dev, Hm, nV = self.device, self.hp_max, self.nV
         f = dict(dtype=torch.float64, device=dev)
         i = dict(dtype=torch.int32, device=dev)
+        tr = None
+        if trace:
+            st, it = self.trace_layout()
+            tr = torch.full((B, it, st), float("nan"), **f)
         return SolveResult(u=torch.zeros(B, nV * Hm, **f), traj=torch.zeros(B, Hm, 2, nV, **f),
                            status=torch.zeros(B, **i), n_scp=torch.zeros(B, **i),
                            n_ipm=torch.zeros(B, **i), obj=torch.zeros(B, **f),
                            max_violation=torch.zeros(B, **f), sum_violations=torch.zeros(B, **f),
                            feasible=torch.zeros(B, **i), n_polish=torch.zeros(B, **i),
-                           n_refine=torch.zeros(B, **i), n_warm=torch.zeros(B, **i))
+                           n_refine=torch.zeros(B, **i), n_warm=torch.zeros(B, **i), trace=tr)
+
+    def _check_out(self, out, B):
+        """Every output buffer must hold B problems' slots on this device (the kernel
+        writes b * slot strides without bounds), contiguous, of the right dtype."""
+        nV, Hm = self.nV, self.hp_max
+        sizes = dict(u=B * nV * Hm, traj=B * Hm * 2 * nV, status=B, n_scp=B, n_ipm=B, obj=B,
+                     max_violation=B, sum_violations=B, feasible=B, n_polish=B, n_refine=B,
+                     n_warm=B)
+        if out.trace is not None:
+            st, it = self.trace_layout()
+            sizes["trace"] = B * st * it
+        for k, n in sizes.items():
+            t = getattr(out, k)
+            want = torch.int32 if k in ("status", "n_scp", "n_ipm", "feasible", "n_polish",
+                                        "n_refine", "n_warm") else torch.float64
+            if t is None:
+                raise ValueError(f"output {k} is missing")
+            if t.device != self.device or t.dtype != want or not t.is_contiguous() or t.numel() < n:
+                raise ValueError(f"output {k}: need a contiguous {want} tensor of >= {n} "
+                                 f"elements on {self.device}")
 
     def linearize(self, x0, u0=None, ec_noise=None, hp=None, obst=None, ref_points=None):
         B, bi, bufs = self._inputs(x0, u0, ec_noise, hp, obst, ref_points, need_obst=False)
@@ -234,6 +285,13 @@ class ScpQpSolver:
                  self.lib)
         torch.cuda.current_stream(self.device).synchronize()
         return ref
+
+
+def _need(t, n, what):
+    """Exact element count of an optional device input (None passes)."""
+    if t is not None and t.numel() != n:
+        raise ValueError(f"{what}: expected {n} elements, got {t.numel()} (shape "
+                         f"{tuple(t.shape)})")
 
 
 def unpack_problem(res, b, nV, hp):

@@ -32,7 +32,7 @@ def test_header_declares_the_boundary():
     fns = header_functions()
     assert fns == sorted(["scpqp_create", "scpqp_destroy", "scpqp_last_error", "scpqp_version",
                           "scpqp_solve", "scpqp_linearize", "scpqp_evaluate",
-                          "scpqp_sample_reference", "scpqp_resources",
+                          "scpqp_sample_reference", "scpqp_resources", "scpqp_trace_layout",
                           "scpqp_delay_compensate", "scpqp_plant_step", "scpqp_clip_controls"])
     assert sorted(LB.EXPORTS) == fns
 

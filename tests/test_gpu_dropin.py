@@ -17,7 +17,14 @@ import Scenarios
 from oracle import scp_reference as R
 from SCP_controller import SCPcontroller
 
+import scp_parity as SP
+
 pytestmark = pytest.mark.gpu
+
+# sign of sum(u[vehicle 0]) of the device's step-0 solve of the noise-free
+# 4-vehicle circle (Hp 20): the mirror branch the kernel's fixed operation order
+# selects at the symmetric cold start
+PINNED_BRANCH_SIGN = -1.0
 
 
 def oracle_for(sc):
@@ -77,7 +84,9 @@ def run_loop(sc, steps):
 
 
 def check_against_oracle(sc, rec, mirror_ok=False):
-    """Same Iter inputs and warm start -> same controller output.
+    """Same Iter inputs and warm start -> same controller output, compared per
+    SCP iteration (device optimization_log vs oracle history) when the SCP
+    counts differ (tests/scp_parity.py).  Returns 'equal', 'flip' or 'mirror'.
 
     ``mirror_ok``: the noise-free circle scenario is mirror-symmetric up to
     fp64 rounding of its initial positions (cos(pi/2) = 6e-17), so at a cold
@@ -85,7 +94,8 @@ def check_against_oracle(sc, rec, mirror_ok=False):
     or all steer right) the iteration settles in is decided by ~1e-15 m
     asymmetries, i.e. by the solver's operation order.  The reference's own
     answer there depends on GUROBI's internal rounding just the same.  For
-    those steps the mirror branch (u -> -u, equal objective) is accepted.
+    those steps the mirror branch (u -> -u, equal objective) is accepted, and
+    the caller pins which branch the device takes.
     """
     o = oracle_for(sc)
     it = rec["Iter"]
@@ -95,16 +105,16 @@ def check_against_oracle(sc, rec, mirror_ok=False):
     # the device sampler against the restatement on the same delay-compensated state
     want_ref = R.reference_points(o, it.x0, sc.Hp)
     assert np.max(np.abs(it.ReferenceTrajectoryPoints - want_ref)) <= 1e-12
-    r = R.scp_solve(p, u_warm=rec["warm"], mode="structured")
+    r = R.scp_solve(p, u_warm=rec["warm"], mode="structured", keep_history=True)
     log = rec["out"]["optimization_log"]
     u = rec["out"]["u"].reshape(-1)
     if mirror_ok and np.max(np.abs(u + r.u)) <= 1e-7 < np.max(np.abs(u - r.u)):
         assert log["obj"] == pytest.approx(r.obj, rel=1e-9)
-        return True
-    if log["n_scp"] == r.n_scp:
-        assert np.max(np.abs(u - r.u)) <= 1e-7
-        assert np.max(np.abs(rec["traj"] - r.traj)) <= 1e-6
-    return log["n_scp"] == r.n_scp
+        return "mirror"
+    res = SP.compare(u, rec["traj"], log["n_scp"], log["trace"], r, sc.nVeh, sc.Hp)
+    # the reference-shaped log lists: one entry per SCP iteration
+    assert len(log["x"]) == len(log["Aineq"]) == log["n_scp"]
+    return "flip" if res["mismatch"] else "equal"
 
 
 def test_circle4_closed_loop():
@@ -113,9 +123,14 @@ def test_circle4_closed_loop():
     sc.get_circle_scenario([2 * math.pi / 4 * (i + 1) for i in range(4)])
     sc.complete_scenario()
     recs = run_loop(sc, 3)
-    agree = [check_against_oracle(sc, r, mirror_ok=(i == 0)) for i, r in enumerate(recs)]
-    assert sum(agree) >= 2
+    kinds = [check_against_oracle(sc, r, mirror_ok=(i == 0)) for i, r in enumerate(recs)]
+    print("circle4 drop-in steps vs restatement:", kinds)
+    assert "mirror" not in kinds[1:]
+    # the branch the device settles in at the symmetric cold start is pinned: its
+    # operation order is fixed, so it is the same on every run (vehicle 0 steers
+    # with the sign recorded here; the restatement's numpy order may pick either)
     r0 = recs[0]
+    assert np.sign(r0["out"]["u"][:20].sum()) == PINNED_BRANCH_SIGN
     assert r0["U"].shape == (20, 4) and r0["traj"].shape == (20, 2, 4)
     assert r0["out"]["u"].shape == (80, 1) and r0["out"]["resultInvalid"] is False
     # QCQP_evaluate at zero input (main.py:197) and evaluateInOriginalProblem (main.py:201)
@@ -177,8 +192,8 @@ def test_frog_single_vehicle_with_obstacles():
     sc.get_frog_scenario()
     sc.complete_scenario()
     recs = run_loop(sc, 2)
-    agree = [check_against_oracle(sc, r) for r in recs]
-    assert all(agree)
+    for r in recs:
+        check_against_oracle(sc, r)
     assert recs[0]["U"].shape == (10, 1)
 
 

@@ -110,38 +110,16 @@ def test_empty_batches(gpu):
 
 
 def test_closed_loop_rollout_matches_restatement(gpu):
-    """Three MPC steps of main.py:98-191 for two realisations (perturbed initial
-    states): delay compensation, warm-started SCP, clipping, plant."""
-    from scpqp.rollout import ClosedLoopBatch
-    sc = R.circle_scenario(4, Hp=10)
-    rng = np.random.default_rng(7)
-    B, steps = 2, 3
-    base = np.array(sc.x0)
-    x_init = base[None] + rng.normal(0, 1, (B, 4, 6)) * np.array([0.05, 0.05, 0.005, 0.02, 0, 0.002])
-    cl = ClosedLoopBatch(sc, B, device=gpu, keep_path=True)
-    cl.reset(x_init)
-    hist = cl.run(steps)
-    for b in range(B):
-        ref = PR.ClosedLoop(sc, x_init=x_init[b])
-        for i in range(steps):
-            r = ref.step(i)
-            h = hist[i]
-            assert np.abs(h["x0"][b].cpu().numpy() - r["x0"]).max() < 1e-6
-            assert np.abs(h["umax"][b].cpu().numpy() - r["umax"]).max() < 1e-12
-            if int(h["n_scp"][b]) == r["n_scp"]:
-                U = h["U"][b].cpu().numpy().reshape(4, 10).T
-                assert np.abs(U - r["U"]).max() < 1e-6
-                path = h["path"][b].cpu().numpy()             # [V, K, 6]
-                tps = sc.ticks_per_sim
-                want = ref.path[:, :, i * tps:(i + 1) * tps + 1].transpose(1, 2, 0)
-                assert np.abs(path - want).max() < 1e-5
-                ev, rev = h["evaluation"], r["evaluation"]     # SCP_controller.py:343-400
-                for k in ("predictionObjectiveValueX", "predictionObjectiveValueU"):
-                    assert abs(float(ev[k][b]) - rev[k]) <= 1e-6 * max(1.0, abs(rev[k]))
-                assert np.abs(ev["constraintValuesVehicle"][b].cpu().numpy()
-                              - rev["constraintValuesVehicle"]).max() < 1e-6
-                assert bool(ev["predictionFeasible"][b]) == rev["predictionFeasible"]
-    cl.close()
+    """Five MPC steps of main.py:98-191 for four realisations (perturbed initial
+    states): every step's solve and plant step on the device's own inputs, and the
+    independent restated loop (tests/closed_loop_check.py; none skipped)."""
+    import closed_loop_check as CC
+    per = CC.run("circle4_hp10", 4, 5, gpu, workers=4)
+    s = CC.summary(per)
+    assert s["solve_kinds"].get("FAIL", 0) == 0 and s["solve_kinds"].get("mirror", 0) == 0
+    assert s["max_plant_err"] <= CC.PLANT_TOL
+    assert s["loop_max_path_diff_same_counts"] <= 1e-5
+    assert s["loop_max_U_diff_same_counts"] <= 1e-6
 
 
 def test_dropin_delay_compensation_matches_straight_line_and_odeint(gpu):
@@ -173,33 +151,32 @@ def test_dropin_delay_compensation_matches_straight_line_and_odeint(gpu):
 def test_closed_loop_rollout_with_obstacles(gpu, kind):
     """Closed loop on the obstacle scenarios (Scenarios.py:127-201): obstacle
     predictions from the constant-velocity obstacle paths (main.py:61-71,
-    MPC_Iter.py:45-51) feed the solve and the evaluation."""
+    MPC_Iter.py:45-51) feed the solve and the evaluation; every step checked on
+    the device's own inputs (tests/closed_loop_check.py)."""
+    import closed_loop_check as CC
+    per = CC.run(kind, 2, 4, gpu, workers=2)
+    s = CC.summary(per)
+    assert s["solve_kinds"].get("FAIL", 0) == 0 and s["solve_kinds"].get("mirror", 0) == 0
+    assert s["max_plant_err"] <= CC.PLANT_TOL
+    assert s["loop_max_path_diff_same_counts"] <= 1e-5
     from scpqp.rollout import ClosedLoopBatch
-    sc = R.frog_scenario(Hp=10) if kind == "frog" else R.parallel_scenario(5, Hp=10)
-    rng = np.random.default_rng(3)
-    B, steps, nV = 2, 2, sc.nVeh
-    x_init = np.array(sc.x0)[None] + rng.normal(0, 1, (B, nV, 6)) * np.array(
-        [0.05, 0.05, 0.005, 0.02, 0, 0.002])
-    cl = ClosedLoopBatch(sc, B, device=gpu, keep_path=True)
+    sc = CC.scenario(kind)
+    x_init = CC.initial_states(kind, 2)
+    cl = ClosedLoopBatch(sc, 2, device=gpu)
     cl.reset(x_init)
-    hist = cl.run(steps)
-    compared = 0
-    for b in range(B):
+    hist = cl.run(2)
+    for b in range(2):
         ref = PR.ClosedLoop(sc, x_init=x_init[b])
-        for i in range(steps):
+        for i in range(2):
             r = ref.step(i)
-            h = hist[i]
-            assert np.abs(h["x0"][b].cpu().numpy() - r["x0"]).max() < 1e-6
-            if int(h["n_scp"][b]) != r["n_scp"]:
+            if int(hist[i]["n_scp"][b]) != r["n_scp"]:
                 break
-            compared += 1
-            U = h["U"][b].cpu().numpy().reshape(nV, 10).T
-            assert np.abs(U - r["U"]).max() < 1e-6
-            ev, rev = h["evaluation"], r["evaluation"]
+            ev, rev = hist[i]["evaluation"], r["evaluation"]     # SCP_controller.py:343-400
             assert bool(ev["predictionFeasible"][b]) == rev["predictionFeasible"]
             assert np.abs(ev["constraintValuesObstacle"][b].cpu().numpy()
                           - rev["constraintValuesObstacle"]).max() < 1e-6
-    assert compared >= 2
+            for k in ("predictionObjectiveValueX", "predictionObjectiveValueU"):
+                assert abs(float(ev[k][b]) - rev[k]) <= 1e-6 * max(1.0, abs(rev[k]))
     cl.close()
 
 

@@ -1,0 +1,148 @@
+"""Device per-SCP-iteration trace (scpqp_batch_out.trace) against the golden
+per-iteration fixtures and the restatement's history.
+
+The reference logs every SCP iterate (SCP_controller.py:169-189: Aineq, bineq,
+x, slack, delta, ...).  The kernel records the same per iteration; these tests
+compare, iteration by iteration:
+
+* replay: one QP from each golden linearisation point hist_u_lin[it] gives the
+  golden rows (hist_A, hist_b, SCP_controller.py:93-128) and QP solution
+  (hist_z, SCP_controller.py:135-150);
+* end to end: the device's own iterates follow the golden history
+  (hist_z, hist_obj, hist_maxviol) and stop at the same iteration.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import scp_reference as R
+from scpqp import batch as BT
+from scpqp import trace as TR
+from scpqp.solver import ScpQpSolver
+
+import scp_parity as SP
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+HIST = {
+    "c1_circle1_hp10": lambda: R.circle_scenario(1, Hp=10),
+    "c2_circle4_hp20": lambda: R.circle_scenario(4, Hp=20),
+    "frog_hp10": lambda: R.frog_scenario(Hp=10),
+    "parallel5_hp10": lambda: R.parallel_scenario(5, Hp=10),
+}
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+
+
+@pytest.mark.parametrize("name", sorted(HIST))
+def test_trace_replays_golden_linearisations(gpu, name):
+    """One QP (max_scp_iter=1) from every recorded linearisation point of golden
+    problem 0: the device's rows equal hist_A/hist_b and its QP solution hist_z."""
+    f = _load(name)
+    sc = HIST[name]()
+    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][0])
+    N = nV * H
+    ul = f["hist_u_lin"]
+    K = ul.shape[0]
+    rep = lambda a: np.repeat(a[0:1], K, axis=0)          # noqa: E731
+    S = ScpQpSolver(sc, max_batch=K, hp_max=int(f["hp_max"]))
+    obst = rep(f["obst"]) if nO else None
+    out = S.solve(rep(f["x0"]), rep(f["u0"]), rep(f["ec_noise"]), obst=obst, u_warm=ul,
+                  max_scp_iter=1, trace=True)
+    lin = S.linearize(rep(f["x0"])[:1], rep(f["u0"])[:1], rep(f["ec_noise"])[:1])
+    torch.cuda.synchronize()
+    g = lin["g"][0].cpu().numpy()[:, :H]
+    tr = out.trace.cpu().numpy()
+    for it in range(K):
+        d = TR.decode(tr[it], 1, nV, nO, H, S.hp_max, g=g, u_lim=S.u_lim)[0]
+        assert np.array_equal(d["u_lin"], ul[it]), it          # the point the rows linearise at
+        A, b = f["hist_A"][it], f["hist_b"][it]
+        if A.shape[0]:
+            sa = max(1.0, np.abs(A).max())
+            assert np.max(np.abs(d["A"] - A)) <= 1e-9 * sa, it
+            assert np.max(np.abs(d["b"] - b)) <= 1e-9 * max(1.0, np.abs(b).max()), it
+        z = f["hist_z"][it]
+        assert np.max(np.abs(d["z"][:N] - z[:N])) <= 1e-8, it   # one QP, same point
+        assert abs(d["slack"] - z[N]) <= 1e-8 * max(1.0, abs(z[N])), it
+        assert d["ipm_iters"] >= 0 and not d["warm"]
+    S.close()
+
+
+@pytest.mark.parametrize("name", sorted(HIST))
+def test_trace_follows_golden_history(gpu, name):
+    """The device's own SCP iterates of golden problem 0 against hist_z / hist_obj /
+    hist_maxviol, iteration by iteration, and the same stopping iteration."""
+    f = _load(name)
+    sc = HIST[name]()
+    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][0])
+    N = nV * H
+    S = ScpQpSolver(sc, max_batch=1, hp_max=int(f["hp_max"]))
+    obst = f["obst"][:1] if nO else None
+    out = S.solve(f["x0"][:1], f["u0"][:1], f["ec_noise"][:1], obst=obst, trace=True)
+    torch.cuda.synchronize()
+    n = int(out.n_scp[0].item())
+    tr = SP.device_trace(out, 0, nV, nO, H, S.hp_max)
+    K = f["hist_z"].shape[0]
+    # the golden history's deltas: obj/maxviol of the iterates, starting from the
+    # evaluation of the (eps-nudged) initial point (SCP_controller.py:77-79, 161)
+    p = R.make_problem(sc, f["x0"][0], f["u0"][0], f["ec_noise"][0], Hp=H,
+                       obst=f["obst"][0].reshape(-1)[:nO * 2 * H].reshape(nO, 2, H))
+    ev0 = R.evaluate_structured(p, R.linearise(p, "structured"), f["hist_u_lin"][0])
+    prev = ev0.obj + R.SLACK_WEIGHT * ev0.max_violation
+    hist = []
+    for it in range(K):
+        cur = float(f["hist_obj"][it]) + R.SLACK_WEIGHT * float(f["hist_maxviol"][it])
+        hist.append(dict(z=f["hist_z"][it], obj=float(f["hist_obj"][it]),
+                         maxviol=float(f["hist_maxviol"][it]), delta=prev - cur))
+        prev = cur
+    assert SP.stops(hist[-1]["delta"], hist[-1]["maxviol"], nV) or K == 20
+    if n != K:
+        class _R:        # the fixture in the shape of an oracle SCPResult
+            n_scp, history = K, hist
+            u = f["u"][0, :N]
+            traj = None
+        SP.compare(None, None, n, tr, _R, nV, H, what=name)
+        K = min(n, K)
+    for it in range(K):
+        assert np.max(np.abs(tr[it]["z"][:N] - f["hist_z"][it][:N])) <= SP.U_TOL, it
+        assert tr[it]["obj"] == pytest.approx(float(f["hist_obj"][it]), rel=1e-9, abs=1e-9)
+        assert tr[it]["maxviol"] == pytest.approx(float(f["hist_maxviol"][it]), rel=1e-7,
+                                                  abs=1e-10)
+        if it + 1 < K:
+            assert np.max(np.abs(tr[it + 1]["u_lin"] - tr[it]["z"][:N])) == 0.0
+    # the final iterate is the returned u
+    assert np.array_equal(tr[-1]["z"][:N], out.u[0, :N].cpu().numpy())
+    assert tr[-1]["obj"] == out.obj[0].item()
+    S.close()
+
+
+def test_trace_does_not_change_results(gpu):
+    """Recording the trace only adds stores: results are bitwise those without it."""
+    sc = R.circle_scenario(4, Hp=20)
+    bt = BT.make_batch(sc, 64, base_seed=77)
+    S = ScpQpSolver(sc, max_batch=64)
+    a = S.solve(bt.x0, bt.u0, bt.ec_noise)
+    ua, na = a.u.clone(), a.n_ipm.clone()
+    b = S.solve(bt.x0, bt.u0, bt.ec_noise, trace=True)
+    torch.cuda.synchronize()
+    assert torch.equal(ua, b.u) and torch.equal(na, b.n_ipm)
+    st, iters = S.trace_layout()
+    assert b.trace.shape == (64, iters, st) and iters == 20
+    # iterations past n_scp are never written (NaN-initialised)
+    ns = b.n_scp.cpu().numpy()
+    tr = b.trace.cpu().numpy()
+    for i in range(64):
+        assert np.all(np.isfinite(tr[i, :ns[i], :8]))
+        assert np.all(np.isnan(tr[i, ns[i]:, 0]))
+    # per-iteration delta reproduces the stopping decision
+    for i in range(64):
+        d = TR.decode(tr[i], int(ns[i]), 4, 0, 20, 20)
+        decided = [SP.stops(x["delta"], x["maxviol"], 4) for x in d]
+        if ns[i] < 20:
+            assert decided[-1] and not any(decided[:-1])
+    S.close()
