@@ -100,11 +100,16 @@ def main():
     ap.add_argument("--hp", type=int, default=20)
     ap.add_argument("--cpu-sample", type=int, default=512)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2",
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2",
                     help="BASELINE config: c2 4 veh Hp 20 B 1024 (the metric's workload, default); "
-                         "c3 8 veh Hp 30 B 4096; c5 4 veh mixed Hp {10,20,30} B 3072")
+                         "c3 8 veh Hp 30 B 4096; c4 4 veh Hp 20, 65536 problems as 8192 per "
+                         "rank (8 GPUs); c5 4 veh mixed Hp {10,20,30} B 3072")
     args = ap.parse_args()
     mixed = None
+    if args.config == "c4":
+        # BASELINE configs[3]: 4 vehicles x 65536 Monte-Carlo realisations, Hp 20, sharded
+        # over 8 GPUs -> 8192 problems per rank
+        args.n_veh, args.hp, args.batch = 4, 20, args.batch if args.batch != 1024 else 8192
     if args.config == "c3":
         args.n_veh, args.hp, args.batch = 8, 30, args.batch if args.batch != 1024 else 4096
         args.cpu_sample = min(args.cpu_sample, 32)
@@ -140,8 +145,10 @@ def main():
     import torch
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        # one rank per GPU; more ranks than GPUs only in a single-box rehearsal of the
+        # sharded path (ranks share a device; SCPQP_DIST_BACKEND=gloo if RCCL refuses it)
+        torch.cuda.set_device(local % torch.cuda.device_count())
+        dist.init_process_group(os.environ.get("SCPQP_DIST_BACKEND", "nccl"))
     else:
         dist = None
         torch.cuda.set_device(0)
@@ -156,6 +163,9 @@ def main():
     stream = torch.cuda.current_stream(dev)
 
     hpt = torch.as_tensor(bt.hp, device=dev) if mixed else None
+    if rank == 0:
+        print(f"bench: {args.config} B={B}/rank x {world} ranks, warmup {args.warmup}, "
+              f"steps {args.steps}", file=sys.stderr, flush=True)
     for _ in range(args.warmup):
         S.solve(x0, u0, ec, hp=hpt, out=out)
     torch.cuda.synchronize()
@@ -180,8 +190,9 @@ def main():
     # end-to-end leg: host (pinned) inputs -> H2D -> solve -> D2H of the result
     # arrays main.py consumes (u, traj, status, obj, max_violation); reported beside `value`,
     # never as it
-    h_in = [t.cpu().pin_memory() for t in (x0, u0, ec)]
-    d_in = [torch.empty_like(t) for t in (x0, u0, ec)]
+    ins = (x0, u0, ec) + ((hpt,) if mixed else ())
+    h_in = [t.cpu().pin_memory() for t in ins]
+    d_in = [torch.empty_like(t) for t in ins]
     outs = (out.u, out.traj, out.status, out.obj, out.max_violation)
     h_out = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in outs]
     e2e_steps = max(min(args.steps, 5), 1)
@@ -190,7 +201,7 @@ def main():
     for _ in range(e2e_steps):
         for d, h in zip(d_in, h_in):
             d.copy_(h, non_blocking=True)
-        S.solve(d_in[0], d_in[1], d_in[2], hp=hpt, out=out)
+        S.solve(d_in[0], d_in[1], d_in[2], hp=d_in[3] if mixed else None, out=out)
         for h, d in zip(h_out, outs):
             h.copy_(d, non_blocking=True)
         torch.cuda.synchronize()
@@ -205,6 +216,8 @@ def main():
     n_warm = out.n_warm.cpu().numpy()
     flops = FL.batch_flops(args.n_veh, bt.hp, 0, n_scp, n_ipm, n_pol, n_ref, n_warm)
     achieved_tf = flops / (kern_ms * 1e-3) / 1e12
+    dense = FL.survey_dense_batch(args.n_veh, bt.hp, 0, n_scp, n_ipm)
+    dense_tf = dense / (kern_ms * 1e-3) / 1e12
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
@@ -236,7 +249,9 @@ def main():
                                f"Hp={'{10,20,30} mixed' if mixed else args.hp}, "
                                f"batch={B} noise seeds per GPU, full SCP solve per problem",
                    "n_veh": args.n_veh, "hp": list(mixed) if mixed else args.hp, "batch_per_gpu": B,
-                   "parallelism": f"{world} independent shards (no collective)"},
+                   "parallelism": (f"{world} of 8 shards of c4's 65536 problems (8192 per rank, "
+                                   f"no collective)" if args.config == "c4" else
+                                   f"{world} independent shards (no collective)")},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "scp_kernel", "kernel_ms": kern_ms,
@@ -245,6 +260,12 @@ def main():
                      "memory_plan": res["plan"], "lds_bytes": res["lds_bytes"],
                      "workgroups": res["grid"],
                      "flops_per_launch": flops,
+                     "flops_note": "executed algorithm (scpqp/flops.py) at the measured counters",
+                     "survey_dense_flops_per_launch": dense,
+                     "survey_dense_achieved": dense_tf,
+                     "survey_dense_frac": dense_tf / FP64_PEAK_TFLOPS,
+                     "survey_dense_note": "SURVEY 8(d) dense-KKT F_ipm at the measured IPM "
+                                          "iteration counts (solver-independent numerator)",
                      "peak_note": "FP64 dense peak (vector = MFMA rate on gfx950, AMD spec)"},
         "qp_solves_per_s": world * float(n_scp.sum()) * args.steps / elapsed,
         "mean_scp_iters": float(n_scp.mean()),
@@ -278,6 +299,8 @@ def main():
                       f"{cpu['cpu_s']:.1f} s of CPU work",
         }
         line["traj_linf_err"] = max(errs) if errs else None
+        line["traj_err_reference"] = ("in-repo CPU restatement of the reference path (oracle/; "
+                                      "CVXOPT/GUROBI absent, parity unpinned: SURVEY 8c)")
         line["traj_err_sample"] = (f"{len(errs)}/{cpu['sample']} problems converged on both sides "
                                    f"with equal SCP iteration count")
         line["traj_linf_err_capped"] = max(capped) if capped else None

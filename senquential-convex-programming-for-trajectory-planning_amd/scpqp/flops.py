@@ -124,6 +124,27 @@ def dense_ipm_reference(n, m):
     return m * n * n + n ** 3 // 3 + 8 * m * n + 4 * n * n
 
 
+def survey_dense_problem(V, H, O, n_scp, n_ipm):
+    """SURVEY.md §8(d)'s solver-independent count of one SCP solve at the measured
+    counts: F_setup + sum_s [F_row + F_eval + k_ipm,s F_ipm(n, m)], with
+    F_ipm(n, m) = m n^2 + n^3/3 + 8 m n + 4 n^2 over the m linearised rows (the
+    formula's m), F_row = 2 V H^2 + m (4H + 8), F_eval = 2 V H^2 + 6 m and
+    F_setup = V (2 F_expm7 + 144 H + 4 H^3), F_expm7 = 14 * 2 * 7^3.  It does not
+    depend on how the kernel solves the QP, so more polish work cannot raise it."""
+    N = V * H
+    n = N + 1
+    m = (V * (V - 1) // 2 + V * O) * H
+    f_row = 2 * V * H * H + m * (4 * H + 8)
+    f_eval = 2 * V * H * H + 6 * m
+    f_setup = V * (2 * 14 * 2 * 7 ** 3 + 144 * H + 4 * H ** 3)
+    return f_setup + n_scp * (f_row + f_eval) + n_ipm * dense_ipm_reference(n, m)
+
+
+def survey_dense_batch(V, hps, O, n_scp, n_ipm):
+    return sum(survey_dense_problem(V, int(H), O, int(s), int(i))
+               for H, s, i in zip(hps, n_scp, n_ipm))
+
+
 def compulsory_bytes(V, H, O):
     """HBM bytes a problem must move: inputs x0, u0, noise (+ obstacles) and outputs u, traj, scalars."""
     N = V * H

@@ -1,0 +1,104 @@
+"""The sharded multi-GPU path executed on the HIP product, with
+world size 2 on the one GPU of the test box (a rehearsal of the 8-GPU node run:
+the ranks share the device).
+
+* two spawned ranks each solve their own shard of the global problem stream
+  through the C-ABI; the gathered results equal one single-process solve of the
+  whole range bit for bit (inputs depend only on the global index);
+* bench.py under torch.distributed.run with two ranks: rank 0 prints one JSON
+  line whose value aggregates both ranks (barrier + max-over-ranks timing).
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PER_RANK = 48
+# RCCL does not take two ranks on one device; the rehearsal's collectives (barrier,
+# max of a scalar, object gather) run on gloo.  On the 8-GPU node bench.py uses nccl.
+BACKEND = "gloo"
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group(BACKEND, rank=rank, world_size=world)
+    try:
+        from oracle import scp_reference as R
+        from scpqp import shard
+        from scpqp.solver import ScpQpSolver
+        torch.cuda.set_device(0)
+        sc = R.circle_scenario(4, Hp=20)
+        bt = shard.shard_batch(sc, PER_RANK, rank, base_seed=5)
+        S = ScpQpSolver(sc, max_batch=PER_RANK, device="cuda:0")
+        out = S.solve(bt.x0, bt.u0, bt.ec_noise)
+        torch.cuda.synchronize()
+        res = (rank, bt.seeds.tolist(), out.u.cpu().numpy(), out.n_scp.cpu().numpy())
+        gathered = [None] * world
+        dist.all_gather_object(gathered, res)
+        tmax = shard.max_over_ranks(1.0 + rank, dist, torch.device("cuda", 0))
+        dist.barrier()
+        S.close()
+        if rank == 0:
+            q.put((gathered, tmax))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_shards_equal_single_solve(gpu):
+    from oracle import scp_reference as R
+    from scpqp import batch as BT
+    from scpqp.solver import ScpQpSolver
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    mp.start_processes(_worker, args=(world, _free_port(), q), nprocs=world, join=True,
+                       start_method="spawn")
+    gathered, tmax = q.get()
+    assert tmax == 2.0
+    sc = R.circle_scenario(4, Hp=20)
+    full = BT.make_batch(sc, world * PER_RANK, base_seed=5)
+    S = ScpQpSolver(sc, max_batch=world * PER_RANK)
+    out = S.solve(full.x0, full.u0, full.ec_noise)
+    torch.cuda.synchronize()
+    seeds, us, ns = [], [], []
+    for rank, s, u, n in sorted(gathered, key=lambda t: t[0]):
+        seeds += s
+        us.append(u)
+        ns.append(n)
+    assert seeds == full.seeds.tolist()
+    assert np.array_equal(np.concatenate(us), out.u.cpu().numpy())
+    assert np.array_equal(np.concatenate(ns), out.n_scp.cpu().numpy())
+    S.close()
+
+
+def test_bench_two_ranks(gpu):
+    env = dict(os.environ, SCPQP_DIST_BACKEND=BACKEND, MASTER_ADDR="127.0.0.1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--batch", "256"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout          # rank 0 only
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["batch_per_gpu"] == 256
+    # value = problems of BOTH ranks / max-over-ranks wall time
+    assert d["value"] == pytest.approx(2 * 256 * 2 / (d["ms_per_step"] * 2 * 1e-3), rel=1e-9)
