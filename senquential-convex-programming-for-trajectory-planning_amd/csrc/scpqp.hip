@@ -67,15 +67,24 @@ __device__ unsigned long long g_ptime[8192 * 2];   // per-problem [start, end] (
         if (threadIdx.x == 0) atomicAdd(&g_prof[cat], _t1 - _pt);                   \
         _pt = _t1;                                                                 \
     } while (0)
+// stamps inside code that only the lead wave runs (panel, triangular solves):
+// counted from that wave's lane 0, whichever wave leads
+#define PROF_ACC_LEAD(cat)                                                         \
+    do {                                                                           \
+        unsigned long long _t1 = __builtin_amdgcn_s_memtime();                      \
+        if ((threadIdx.x & 63) == 0) atomicAdd(&g_prof[cat], _t1 - _pt);            \
+        _pt = _t1;                                                                 \
+    } while (0)
 #else
 #define PROF_T0() (void)0
 #define PROF_ACC(cat) (void)0
+#define PROF_ACC_LEAD(cat) (void)0
 #endif
 // Fine-grained stamps inside the factorisation (panel sub-phases, barrier waits):
 // only with -DSCPQP_PROF_FINE, since their atomics perturb whole-batch timelines.
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
 #define PROF_T0_FINE() PROF_T0()
-#define PROF_ACC_FINE(cat) PROF_ACC(cat)
+#define PROF_ACC_FINE(cat) PROF_ACC_LEAD(cat)
 #else
 #define PROF_T0_FINE() (void)0
 #define PROF_ACC_FINE(cat) (void)0
@@ -206,6 +215,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
 template <bool HG, bool VG, int RM, int OCC>
 struct Lay {
     static constexpr int RMAX = RM;   // row slots of the triangular solves (n <= 64 RM)
+    static constexpr bool HGLOBAL = HG;   // the factor lives in the global workspace
     using HT = typename std::conditional<HG, gdouble, ldouble>::type;
     using VT = typename std::conditional<VG, gdouble, ldouble>::type;
     int V, O, Hb, N, n, m, mc, ld, mp, nb;
@@ -1100,13 +1110,16 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         }
     }
     PROF_ACC_FINE(20);
+    // 16-byte pair stores: the pair (c, c + 1) of row i is inside the row or its
+    // even-length padding whenever r0 + c <= i (r0 and c even), and column n of the
+    // last row is the spare row the plan allocates
 #pragma unroll
     for (int t = 0; t < RS; ++t) {
         const int i = r0 + lane + 64 * t;
         if (i < n) {
 #pragma unroll
-            for (int c = 0; c < CB; ++c)
-                if (c < jb && c <= lane + 64 * t) H[ro[t] + r0 + c] = p[t][c];
+            for (int c = 0; c < CB; c += 2)
+                if (c < jb && c <= lane + 64 * t) st2(H + ro[t] + r0 + c, double2v{p[t][c], p[t][c + 1]});
         }
     }
     if (lane == 0) flag[0] = bad;
@@ -1164,6 +1177,57 @@ __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, con
     }
 }
 
+// The same rank-CB trailing update on the matrix cores, for a factor that lives in
+// the global workspace (plan 2: 8 vehicles at Hp 30, n = 241).  There the VALU
+// update is the factorisation's critical path (the lead wave waits ~95 % of each
+// panel step at the barrier, profiles/r02_phases_fine.txt): 2 x 2 register tiles
+// re-read their operands from L2 for every 4 outputs.  Here a wave takes whole
+// 16 x 16 tiles (i >= k): K_ik -= sum_c (L_ic D_c) L_kc is two
+// v_mfma_f64_16x16x4_f64 (CB = 8 = 2 x 4) with the old tile as the accumulator
+// and the A operand negated, so the tile is loaded once and stored once.
+// Operand layouts (gfx950): A[row = lane & 15][k = lane >> 4], B[k = lane >> 4]
+// [col = lane & 15], C/D col = lane & 15, row = (lane >> 4) + 4 r.  Entries above
+// the diagonal of a diagonal tile and outside the matrix are neither read nor
+// written (packed rows end at the diagonal).
+typedef double double4v __attribute__((ext_vector_type(4)));
+#ifndef SCPQP_MFMA_TRAIL
+#define SCPQP_MFMA_TRAIL 1
+#endif
+template <class HP>
+__device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
+                                                     int wave, int nwave) {
+    static_assert(CB == 8, "two 16x16x4 MFMAs per tile");
+    const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
+    const double d0 = dcur[lk], d1 = dcur[4 + lk];
+    const int T = (n - r1 + 15) >> 4;
+    const int ntile = T * (T + 1) / 2;
+    for (int t = wave; t < ntile; t += nwave) {
+        int I, J;
+        tri_decode(t, I, J);
+        const int i0 = r1 + 16 * I, k0 = r1 + 16 * J;
+        const int ia = min(i0 + lr, n - 1), kb = min(k0 + lr, n - 1);
+        const int oa = roff(ia) + j0, ob = roff(kb) + j0;
+        const double a0 = -H[oa + lk] * d0, a1 = -H[oa + 4 + lk] * d1;
+        const double b0 = H[ob + lk], b1 = H[ob + 4 + lk];
+        const int kc = k0 + lr;
+        double4v acc;
+        int oc[4];
+        bool ok[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int ci = i0 + lk + 4 * r;
+            ok[r] = ci < n && kc <= ci;
+            oc[r] = roff(ok[r] ? ci : 0) + (ok[r] ? kc : 0);
+            acc[r] = ok[r] ? (double)H[oc[r]] : 0.0;
+        }
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc, 0, 0, 0);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (ok[r]) H[oc[r]] = acc[r];
+    }
+}
+
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int n = __builtin_amdgcn_readfirstlane(L.n);
@@ -1182,16 +1246,20 @@ __device__ bool cholesky(const LT& L) {
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
         } else if (jp >= 0 && r1 < n) {
-            trailing_update(L.H, n, jp, r1, dprev,
-                            ((wave_id() - L.lead + 3) & 3) * 64 + (int)(threadIdx.x & 63), NT - 64);
+            const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
+            if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL)
+                trailing_update_mfma(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
+            else
+                trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
         }
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
         unsigned long long _pb = __builtin_amdgcn_s_memtime();
 #endif
         __syncthreads();
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
-        if (threadIdx.x == 0) atomicAdd(&g_prof[22], __builtin_amdgcn_s_memtime() - _pb);
-        if (threadIdx.x == 64) atomicAdd(&g_prof[23], __builtin_amdgcn_s_memtime() - _pb);
+        // barrier waits of the lead wave (panel chain) and of one trailing-update wave
+        if (threadIdx.x == 64 * L.lead) atomicAdd(&g_prof[22], __builtin_amdgcn_s_memtime() - _pb);
+        if (threadIdx.x == 64 * ((L.lead + 1) & 3)) atomicAdd(&g_prof[23], __builtin_amdgcn_s_memtime() - _pb);
 #endif
         if (flag[par]) return false;
     }
@@ -1200,11 +1268,15 @@ __device__ bool cholesky(const LT& L) {
 }
 
 // ---------------------------------------------------------------------------
-// Solve K x = b with K = L D L'.  Wave 0 only; rows i = lane + 64 t (t < R).
+// Solve K x = b with K = L D L'.  The lead wave only; rows i = lane + 64 t (t < R).
 // Unit-lower forward / backward substitution: the dependency chain per step
 // is one v_readlane broadcast of the owner lane's value plus one FMA.  L is
-// streamed 8 columns (forward) / 8 rows (backward) at a time into registers,
+// streamed 4 columns (forward) / 4 rows (backward) at a time into registers,
 // double-buffered, so the LDS latency hides behind the dependent steps.
+// (Measured alternatives, tools/probe/solve_probe.hip and DESIGN §3: ping-pong
+// buffers with bounds-free full chunks, v_writelane capture, and a blocked
+// variant that solves 8 x 8 diagonal blocks on uniform values; the first two
+// are faster in isolation but slower inside the kernel, the third is slower.)
 // ---------------------------------------------------------------------------
 
 template <int R, class HP>
@@ -2285,8 +2357,11 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Host side
+// Host side (left out of device-only probe builds: tools/probe/)
 // ---------------------------------------------------------------------------
+#ifdef SCPQP_NO_HOST
+}  // namespace
+#else
 thread_local char g_err[512] = "";
 
 int fail(int code, const char* fmt, const char* detail = "") {
@@ -2640,3 +2715,4 @@ int scpqp_resources(scpqp_handle* h, int64_t* lds, int64_t* ws, int32_t* big, in
 }
 
 }  // extern "C"
+#endif  // SCPQP_NO_HOST

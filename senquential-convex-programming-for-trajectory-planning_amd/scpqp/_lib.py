@@ -91,7 +91,8 @@ def load(path=None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = path or LIB_PATH
+    # SCPQP_LIB: a diagnostic build of the same library (A/B runs of kernel variants)
+    p = path or os.environ.get("SCPQP_LIB") or LIB_PATH
     if not os.path.exists(p):
         raise OSError(f"scpqp: HIP library not built ({p}); run __graft_entry__.build()")
     lib = C.CDLL(p)
