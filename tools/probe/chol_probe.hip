@@ -11,6 +11,7 @@ template <int R>
 struct PLay {
     static constexpr int RMAX = R;
     static constexpr bool HGLOBAL = false;
+    static constexpr int OCCV = 3;
     ldouble *H, *dinv, *red;
     int n, lead;
 };
