@@ -202,10 +202,20 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     int u = 0, w = 0;
     // packed K plus one spare row (row n: target of the predicate-free tile stores)
     if (hG) { f.H = w; w += pad2(roff(n + 1) + 16); } else { f.H = p + u; u += pad2(roff(n + 1) + 16); }
-    f.Wt = p + u; u += pad2(4 * Hm * nb);
-    if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     const int setup = NWAVE * SCR_PER_WAVE;
+    // plan 2 with constraint-row arrays at least as large as the setup scratch (8
+    // vehicles at Hp 30): the W~ blocks go to the workspace as well, and the setup
+    // scratch (expm, dead before the first linearisation) shares the row arrays, so
+    // the union is empty and two workgroups fit per CU
+    const bool wG = hG && vG && (n + 63) / 64 == 4;   // = Lay::WGLOBAL
+    const bool rows_scr = wG && f.rinfo + pad2((m + 1) / 2) - f.rowE >= setup;
+    if (wG) { f.Wt = w; w += pad2(4 * Hm * nb); } else { f.Wt = p + u; u += pad2(4 * Hm * nb); }
+    if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     f.uni = u > setup ? u : setup;
+    if (rows_scr) {
+        f.scr = f.rowE;
+        f.uni = 0;
+    }
     f.ws = w;
     f.ldAlloc = ld;
     f.mcAlloc = pad2(mc);
@@ -222,7 +232,11 @@ struct Lay {
     int V, O, Hb, N, n, m, mc, ld, mp, nb;
     int lead;   // the wave that runs the serial parts (panel, triangular solves)
     ldouble *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
-    ldouble *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr, *Wt;
+    ldouble *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr;
+    // W~ blocks: in the workspace on plan 2 for factors of 4 row slots (plan_offsets)
+    static constexpr bool WGLOBAL = HG && VG && RM == 4;
+    using WT = typename std::conditional<WGLOBAL, gdouble, ldouble>::type;
+    WT* Wt;
     lint* rinfo;
     HT* H;
     VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
@@ -244,7 +258,8 @@ __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* 
     L.ya = lds + f.ya; L.yb = lds + f.yb; L.qs = lds + f.qs; L.rowE = lds + f.rowE;
     L.rowW = lds + f.rowW; L.rowH = lds + f.rowH; L.z = lds + f.z; L.dz = lds + f.dz;
     L.rhs = lds + f.rhs; L.rd = lds + f.rd; L.dinv = lds + f.dinv; L.red = lds + f.red;
-    L.scr = lds + f.scr; L.Wt = lds + f.Wt;
+    L.scr = lds + f.scr;
+    if constexpr (Lay<HG, VG, RM, OCC>::WGLOBAL) L.Wt = ws + f.Wt; else L.Wt = lds + f.Wt;
     L.rinfo = (lint*)(lds + f.rinfo);
     if constexpr (HG) L.H = ws + f.H; else L.H = lds + f.H;
     typename Lay<HG, VG, RM, OCC>::VT* vb;
@@ -914,7 +929,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
                 w01 = dr * e0 * e1;
                 w11 = dr * e1 * e1;
             }
-            ldouble* W = L.Wt + 4 * e;
+            auto* W = L.Wt + 4 * e;
             W[0] = w00; W[1] = w01; W[2] = w01; W[3] = w11;
         } else {
             const int q = e - nW, v = q / Hb, k = q % Hb;
@@ -948,7 +963,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
         const int l0 = 2 * lt, m0 = 2 * mt;
         const ldouble* ga = L.g + a_ * Hb * 2;
         const ldouble* gb = L.g + b_ * Hb * 2;
-        const ldouble* W = L.Wt + 4 * (a_ * (a_ + 1) / 2 + b_);
+        const auto* W = L.Wt + 4 * (a_ * (a_ + 1) / 2 + b_);
         double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
         for (int k = l0 > m0 ? l0 : m0; k < Hb; ++k) {
             const double2v a0 = ld2(ga + (k - l0) * 2);
@@ -2399,6 +2414,18 @@ int scpqp_wide_launch(const void* args, int grid, size_t lds, void* stream) {
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, static_cast<hipStream_t>(stream), a);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+#ifdef SCPQP_PROF
+// this translation unit's phase counters (the diagnostic reader adds them)
+extern "C" int scpqp_wide_prof_read(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[24] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
 #endif
 #else
 thread_local char g_err[512] = "";
@@ -2469,8 +2496,9 @@ int plan(scpqp_handle* h) {
     h->wsStride = f.ws;
     h->grid = h->cus * bestPer;
     h->occ = bestPer >= 3 ? 3 : 2;
-    // factors of 4 row slots on plan 2 (one workgroup per CU): the 8-wave kernel
-    if (best == 2 && (V * Hm + 1 + 63) / 64 == 4 && !getenv("SCPQP_NO_WIDE")) {
+    // factors of 4 row slots on plan 2 at one workgroup per CU: the 8-wave kernel
+    if (best == 2 && (bestPer == 1 || getenv("SCPQP_FORCE_WIDE")) && (V * Hm + 1 + 63) / 64 == 4 &&
+        !getenv("SCPQP_NO_WIDE")) {
         const size_t lds = (size_t)scpqp_wide_lds_bytes(V, O, Hm);
         if (lds <= kLdsLimit) {
             h->wide = 1;
@@ -2503,7 +2531,11 @@ int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
 int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     if (a.B <= 0) return 0;
     HIPCHK(hipSetDevice(h->device));
-    const int grid = a.B < h->grid ? a.B : h->grid;
+    int grid = a.B < h->grid ? a.B : h->grid;
+    if (const char* g = getenv("SCPQP_GRID")) {   // diagnostic: fewer resident workgroups
+        const int cap = atoi(g);
+        if (cap > 0 && cap < grid) grid = cap;
+    }
     if (h->wsStride > 0) {
         const size_t need = (size_t)grid * h->wsStride * sizeof(double);
         if (need > h->wsBytes) {
@@ -2746,8 +2778,12 @@ int scpqp_prof_times(unsigned long long* out, int n) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptime), sizeof(unsigned long long) * 2 * n));
     return 0;
 }
+int scpqp_wide_prof_read(unsigned long long* out, int reset);
 int scpqp_prof_read(unsigned long long* out, int reset) {
+    unsigned long long w[24];
+    if (scpqp_wide_prof_read(w, reset) != 0) return fail(SCPQP_E_HIP, "prof read%s");
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24));
+    for (int i = 0; i < 24; ++i) out[i] += w[i];
     if (reset) {
         unsigned long long z[24] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
