@@ -39,7 +39,9 @@ import numpy as np  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD datasheet
 HBM_PEAK_GBS = 8000.0
 METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu_round2.sh + pmc_summary.py)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic_{}.json")
+PMC_SQ = os.path.join(ROOT, "profiles", "r02_pmc_sq_c2.json")
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -222,14 +224,22 @@ def main():
     value = world * B * args.steps / elapsed
 
     # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # workload (tools/gpu_round.sh + tools/pmc_summary.py); measured on c2 only
-    traffic = None
-    if args.config == "c2" and B == 1024 and os.path.exists(PMC_SUMMARY):
+    # workload at its default batch (tools/gpu_round2.sh + tools/pmc_summary.py)
+    traffic, sq = None, None
+    default_b = {"c2": 1024, "c3": 4096, "c4": 8192, "c5": 3072}[args.config]
+    tpath = PMC_TRAFFIC.format(args.config)
+    if B == default_b and os.path.exists(tpath):
         try:
-            with open(PMC_SUMMARY) as fh:
+            with open(tpath) as fh:
                 traffic = json.load(fh).get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    if args.config == "c2" and B == default_b and os.path.exists(PMC_SQ):
+        try:
+            with open(PMC_SQ) as fh:
+                sq = json.load(fh)
+        except (OSError, ValueError):
+            sq = None
     res = S.resources()
 
     line = {
@@ -255,8 +265,14 @@ def main():
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "scp_kernel", "kernel_ms": kern_ms,
-                     "traffic_source": "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE)"
+                     "traffic_source": f"profiles/{os.path.basename(tpath)} (FETCH_SIZE x2 + WRITE_SIZE)"
                      if traffic is not None else None,
+                     "hbm_achieved_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
+                     "hbm_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
+                     "lds_bank_conflict_ratio": sq["lds_bank_conflict_ratio"] if sq else None,
+                     "sq_wait_any_frac": sq["wait_any_frac"] if sq else None,
+                     "sq_source": f"profiles/{os.path.basename(PMC_SQ)} (SQ_LDS_BANK_CONFLICT / "
+                                  f"SQ_LDS_IDX_ACTIVE, SQ_WAIT_ANY / SQ_WAVE_CYCLES)" if sq else None,
                      "memory_plan": res["plan"], "lds_bytes": res["lds_bytes"],
                      "workgroups": res["grid"],
                      "flops_per_launch": flops,

@@ -1017,7 +1017,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
 #define SCPQP_CB 8
 #endif
 #define CB SCPQP_CB
-static_assert(CB % 2 == 0 && CB <= 8, "pivot double buffer holds 2 x 8 entries");
+static_assert(CB % 4 == 0 && CB <= 8, "pivot double buffer holds 2 x 8 entries");
 
 // 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
 // a fraction of the IEEE division sequence's latency on the serial panel path).
@@ -1210,19 +1210,22 @@ typedef double double4v __attribute__((ext_vector_type(4)));
 #define SCPQP_MFMA_TRAIL 1
 #endif
 
-// U tiles are in flight per wave so that their L2 loads overlap: 4 at one workgroup
-// per CU (256 VGPRs; c3 2.37k -> 2.73k solves/s), 2 at three (168 VGPRs; more
-// spill, c5 -3.5 % at 4), tools/gpu_ab_libs.sh.
+// U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
+// budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
+// tools/gpu_ab_libs.sh.
 template <int U, class HP>
 __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
                                                      int wave, int nwave) {
-    static_assert(CB == 8, "two 16x16x4 MFMAs per tile");
+    static_assert(CB % 4 == 0, "CB / 4 16x16x4 MFMAs per tile");
+    constexpr int KS = CB / 4;
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
-    const double d0 = dcur[lk], d1 = dcur[4 + lk];
+    double dk[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) dk[kk] = dcur[4 * kk + lk];
     const int T = (n - r1 + 15) >> 4;
     const int ntile = T * (T + 1) / 2;
     for (int t = wave; t < ntile; t += U * nwave) {
-        double a0[U], a1[U], b0[U], b1[U];
+        double a[U][KS], b[U][KS];
         double4v acc[U];
         int oc[U][4];
         bool ok[U][4];
@@ -1235,10 +1238,11 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
             const int i0 = r1 + 16 * I, k0 = r1 + 16 * J;
             const int ia = min(i0 + lr, n - 1), kb = min(k0 + lr, n - 1);
             const int oa = roff(ia) + j0, ob = roff(kb) + j0;
-            a0[u] = -H[oa + lk] * d0;
-            a1[u] = -H[oa + 4 + lk] * d1;
-            b0[u] = H[ob + lk];
-            b1[u] = H[ob + 4 + lk];
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk) {
+                a[u][kk] = -H[oa + 4 * kk + lk] * dk[kk];
+                b[u][kk] = H[ob + 4 * kk + lk];
+            }
             const int kc = k0 + lr;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -1250,8 +1254,9 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0[u], b0[u], acc[u], 0, 0, 0);
-            acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1[u], b1[u], acc[u], 0, 0, 0);
+#pragma unroll
+            for (int kk = 0; kk < KS; ++kk)
+                acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][kk], b[u][kk], acc[u], 0, 0, 0);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -1281,7 +1286,7 @@ __device__ bool cholesky(const LT& L) {
         } else if (jp >= 0 && r1 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL)
-                trailing_update_mfma<LT::OCCV >= 3 ? 2 : 4>(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
+                trailing_update_mfma<(LT::OCCV >= 3 ? 16 : 32) / CB>(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
             else
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
         }
@@ -2394,39 +2399,6 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
 // ---------------------------------------------------------------------------
 #ifdef SCPQP_NO_HOST
 }  // namespace
-#ifdef SCPQP_WIDE_TU
-// The library's second translation unit (csrc/scpqp_wide.hip, SCPQP_NT = 512): the
-// plan-2 kernel for factors of 4 row slots (n > 192: 8 vehicles at Hp 30) with 8
-// waves per workgroup at one workgroup per CU (256 VGPRs, as the 4-wave build at
-// 2 per CU).  That configuration runs one workgroup per CU anyway (LDS), and its
-// factorisation is bound by the trailing update: 7 waves share it instead of 3.
-int scpqp_wide_lds_bytes(int V, int O, int Hm) {
-    const Off f = plan_offsets(V, O, Hm, true, true);
-    return (f.persist + f.uni) * (int)sizeof(double);
-}
-int scpqp_wide_launch(const void* args, int grid, size_t lds, void* stream) {
-    KArgs a;
-    memcpy(&a, args, sizeof(a));
-    auto kern = scp_kernel<true, true, 4, 1>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return -2;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), lds, static_cast<hipStream_t>(stream), a);
-    return hipGetLastError() == hipSuccess ? 0 : -2;
-}
-#ifdef SCPQP_PROF
-// this translation unit's phase counters (the diagnostic reader adds them)
-extern "C" int scpqp_wide_prof_read(unsigned long long* out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24) != hipSuccess)
-        return -2;
-    if (reset) {
-        unsigned long long z[24] = {0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)) != hipSuccess) return -2;
-    }
-    return 0;
-}
-#endif
-#endif
 #else
 thread_local char g_err[512] = "";
 
@@ -2443,13 +2415,8 @@ int fail(int code, const char* fmt, const char* detail = "") {
 
 }  // namespace
 
-// csrc/scpqp_wide.hip (the 8-wave plan-2 kernel, see SCPQP_WIDE_TU)
-int scpqp_wide_lds_bytes(int V, int O, int Hm);
-int scpqp_wide_launch(const void* args, int grid, size_t lds, void* stream);
-
 struct scpqp_handle {
     scpqp_dims dims;
-    int wide = 0;   // launch the 8-wave plan-2 kernel (scpqp_wide_launch)
     DevParams hostP;
     DevParams* devP = nullptr;
     int device = 0;
@@ -2496,16 +2463,6 @@ int plan(scpqp_handle* h) {
     h->wsStride = f.ws;
     h->grid = h->cus * bestPer;
     h->occ = bestPer >= 3 ? 3 : 2;
-    // factors of 4 row slots on plan 2 at one workgroup per CU: the 8-wave kernel
-    if (best == 2 && (bestPer == 1 || getenv("SCPQP_FORCE_WIDE")) && (V * Hm + 1 + 63) / 64 == 4 &&
-        !getenv("SCPQP_NO_WIDE")) {
-        const size_t lds = (size_t)scpqp_wide_lds_bytes(V, O, Hm);
-        if (lds <= kLdsLimit) {
-            h->wide = 1;
-            h->ldsBytes = lds;
-            h->grid = h->cus;   // one 512-thread workgroup per CU
-        }
-    }
 #ifdef SCPQP_OCC4
     // diagnostic build: 4 workgroups per CU on plan 2 (matrix and vectors in the
     // workspace), register budget compiled for 4 (128 VGPRs)
@@ -2550,11 +2507,6 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.wsStride = h->wsStride;
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
-    if (h->wide) {
-        if (scpqp_wide_launch(&a, grid, h->ldsBytes, st) != 0)
-            return fail(SCPQP_E_HIP, "HIP error: %s", hipGetErrorString(hipGetLastError()));
-        return 0;
-    }
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
     const int occ = h->occ;   // workgroups per CU the register budget is compiled for
 #ifdef SCPQP_OCC4
@@ -2778,12 +2730,8 @@ int scpqp_prof_times(unsigned long long* out, int n) {
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ptime), sizeof(unsigned long long) * 2 * n));
     return 0;
 }
-int scpqp_wide_prof_read(unsigned long long* out, int reset);
 int scpqp_prof_read(unsigned long long* out, int reset) {
-    unsigned long long w[24];
-    if (scpqp_wide_prof_read(w, reset) != 0) return fail(SCPQP_E_HIP, "prof read%s");
     HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24));
-    for (int i = 0; i < 24; ++i) out[i] += w[i];
     if (reset) {
         unsigned long long z[24] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));

@@ -9,7 +9,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)
 _REPO = os.path.dirname(_ROOT)
 SRC = os.path.join(_ROOT, "csrc", "scpqp.hip")
-SRCS = [SRC, os.path.join(_ROOT, "csrc", "scpqp_wide.hip"), os.path.join(_ROOT, "csrc", "plant.hip")]
+SRCS = [SRC, os.path.join(_ROOT, "csrc", "plant.hip")]
 INCLUDE = os.path.join(_REPO, "include")
 LIB_PATH = os.path.join(_PKG, "libscpqp.so")
 ARCH = os.environ.get("SCPQP_ARCH", "gfx950")
