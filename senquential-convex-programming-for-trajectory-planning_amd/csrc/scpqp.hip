@@ -1049,7 +1049,8 @@ __device__ __forceinline__ bool is_lead(int lead) { return wave_id() == lead; }
 // the diagonal (lane < c) only hold values that are never broadcast or stored.
 template <int RS, class HP>
 __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
-                                             const ldouble* dprev, ldouble* dout, lint* flag) {
+                                             const ldouble* dprev, ldouble* dout, lint* flag,
+                                             int nprev = 1) {
     const int lane = threadIdx.x & 63;
     PROF_T0_FINE();
     double p[RS][CB];
@@ -1069,21 +1070,22 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
     __builtin_amdgcn_s_waitcnt(0);
 #endif
     PROF_ACC_FINE(18);
-    if (jp >= 0) {
-        // look-ahead update p_ic -= sum_c' L_ic' (D_c' L_{r0+c, c'}).  Row r0 + c of
-        // the previous panel is lane c's own row (slot 0), so its D-scaled entries
-        // are broadcast with v_readlane instead of a serialised LDS broadcast load
+    // look-ahead update p_ic -= sum_c' L_ic' (D_c' L_{r0+c, c'}) from the nprev
+    // panels starting at column jp (two when the trailing update is paired).  Row
+    // r0 + c of a previous panel is lane c's own row (slot 0), so its D-scaled
+    // entries are broadcast with v_readlane instead of a serialised LDS broadcast load
+    for (int q = 0; jp >= 0 && q < nprev; ++q) {
         double li[RS][CB], ld[CB];
 #pragma unroll
         for (int t = 0; t < RS; ++t)
 #pragma unroll
             for (int c = 0; c < CB; c += 2) {
-                const double2v v = ld2(H + ro[t] + jp + c);
+                const double2v v = ld2(H + ro[t] + jp + q * CB + c);
                 li[t][c] = v.x;
                 li[t][c + 1] = v.y;
             }
 #pragma unroll
-        for (int c = 0; c < CB; ++c) ld[c] = li[0][c] * dprev[c];
+        for (int c = 0; c < CB; ++c) ld[c] = li[0][c] * dprev[q * CB + c];
 #pragma unroll
         for (int c = 0; c < CB; ++c) {
             double lk[CB];
@@ -1200,7 +1202,8 @@ __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, con
 // re-read their operands from L2 for every 4 outputs.  Here a wave takes whole
 // 16 x 16 tiles (i >= k): K_ik -= sum_c (L_ic D_c) L_kc is two
 // v_mfma_f64_16x16x4_f64 (CB = 8 = 2 x 4) with the old tile as the accumulator
-// and the A operand negated, so the tile is loaded once and stored once.
+// and the A operand negated, so the tile is loaded once and stored once.  KS
+// 16x16x4 MFMAs per tile: the update's rank is 4 KS (CB, or 2 CB when paired).
 // Operand layouts (gfx950): A[row = lane & 15][k = lane >> 4], B[k = lane >> 4]
 // [col = lane & 15], C/D col = lane & 15, row = (lane >> 4) + 4 r.  Entries above
 // the diagonal of a diagonal tile and outside the matrix are neither read nor
@@ -1213,11 +1216,9 @@ typedef double double4v __attribute__((ext_vector_type(4)));
 // U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
 // budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
 // tools/gpu_ab_libs.sh.
-template <int U, class HP>
+template <int U, int KS, class HP>
 __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
                                                      int wave, int nwave) {
-    static_assert(CB % 4 == 0, "CB / 4 16x16x4 MFMAs per tile");
-    constexpr int KS = CB / 4;
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     double dk[KS];
 #pragma unroll
@@ -1266,29 +1267,49 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
     }
 }
 
+// Paired trailing update (factor in the global workspace): the update streams
+// the whole remaining factor through L2 once per application, and for n = 241 it
+// is the factorisation's critical path.  The trailing waves therefore apply the
+// rank-2CB update of two panels at once, on even panel steps, and idle on odd
+// ones; the lead's look-ahead covers both panels on even steps.  Half the passes
+// over the factor, at the price of one exposed panel chain per pair.
+#ifndef SCPQP_PAIR
+#define SCPQP_PAIR 1
+#endif
+
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int n = __builtin_amdgcn_readfirstlane(L.n);
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
-    lint* flag = (lint*)(L.red + 120);   // [parity]
-    ldouble* dbuf = L.red + 64;          // pivots [parity][CB]
+    constexpr bool PAIR = LT::HGLOBAL && SCPQP_MFMA_TRAIL && SCPQP_PAIR;
+    lint* flag = (lint*)(L.red + 120);   // [step parity]
+    ldouble* dbuf = L.red + 64;          // pivots [step mod 4][CB]; a pair's slots are adjacent
     PROF_T0();
-    for (int r0 = 0, par = 0; r0 < n; r0 += CB, par ^= 1) {
-        const int jp = r0 - CB;   // previous panel (none at the first step)
+    for (int r0 = 0, s = 0; r0 < n; r0 += CB, ++s) {
+        const int par = s & 1;
         const int jb = min(CB, n - r0), r1 = r0 + jb;
-        const ldouble* dprev = dbuf + (par ^ 1) * CB;
+        // look-ahead source: the previous panel, or the previous pair on even paired steps
+        const int np = (PAIR && par == 0 && s >= 2) ? 2 : 1;
+        const int jp = r0 - np * CB;   // < 0 at the first step: no look-ahead
+        const ldouble* dprev = dbuf + ((s - np) & 3) * CB;
         if (is_lead(L.lead)) {
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
-            ldouble* dn = dbuf + par * CB;
-            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
-            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par);
+            ldouble* dn = dbuf + (s & 3) * CB;
+            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
+            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
         } else if (jp >= 0 && r1 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
-            if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL)
-                trailing_update_mfma<(LT::OCCV >= 3 ? 16 : 32) / CB>(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
-            else
+            if constexpr (PAIR) {
+                if (np == 2)
+                    trailing_update_mfma<(LT::OCCV >= 3 ? 2 : 4), 2 * CB / 4>(L.H, n, jp, r1, dprev, tw,
+                                                                               NWAVE - 1);
+            } else if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
+                trailing_update_mfma<(LT::OCCV >= 3 ? 16 : 32) / CB, CB / 4>(L.H, n, jp, r1, dprev, tw,
+                                                                           NWAVE - 1);
+            } else {
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
+            }
         }
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
         unsigned long long _pb = __builtin_amdgcn_s_memtime();
