@@ -196,7 +196,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.rhs = p; p += pad2(n);
     f.rd = p; p += pad2(n);
     f.dinv = p; p += pad2(n);
-    f.red = p; p += 128;   // [0,64) reductions, [64,80) panel pivots, 120 flag, 124 work slot
+    f.red = p; p += 192;   // [0,64) reductions, 120 flag, 124 work slot, 126 lead, [128,192) pivots
     f.persist = p;
     f.scr = p;
     int u = 0, w = 0;
@@ -1017,7 +1017,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
 #define SCPQP_CB 8
 #endif
 #define CB SCPQP_CB
-static_assert(CB % 4 == 0 && CB <= 8, "pivot double buffer holds 2 x 8 entries");
+static_assert(CB % 4 == 0 && CB <= 8, "panel width");
 
 // 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
 // a fraction of the IEEE division sequence's latency on the serial panel path).
@@ -1267,46 +1267,47 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
     }
 }
 
-// Paired trailing update (factor in the global workspace): the update streams
+// Grouped trailing update (factor in the global workspace): the update streams
 // the whole remaining factor through L2 once per application, and for n = 241 it
 // is the factorisation's critical path.  The trailing waves therefore apply the
-// rank-2CB update of two panels at once, on even panel steps, and idle on odd
-// ones; the lead's look-ahead covers both panels on even steps.  Half the passes
-// over the factor, at the price of one exposed panel chain per pair.
-#ifndef SCPQP_PAIR
-#define SCPQP_PAIR 1
+// rank-(G CB) update of G panels at once, on steps s = 0 mod G, and idle on the
+// others; the lead's look-ahead covers every panel factored since the last group
+// update.  1/G of the passes over the factor, at the price of G - 1 exposed panel
+// chains per group (G = 2: c3 3.51-3.55k -> 4.04-4.07k solves/s).
+#ifndef SCPQP_GROUP
+#define SCPQP_GROUP 2
 #endif
+static_assert(SCPQP_GROUP == 1 || SCPQP_GROUP == 2 || SCPQP_GROUP == 4, "group of 1, 2 or 4 panels");
+static_assert(2 * SCPQP_GROUP * CB <= 64, "the pivot buffer holds 64 entries");
 
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int n = __builtin_amdgcn_readfirstlane(L.n);
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
-    constexpr bool PAIR = LT::HGLOBAL && SCPQP_MFMA_TRAIL && SCPQP_PAIR;
+    constexpr int G = (LT::HGLOBAL && SCPQP_MFMA_TRAIL) ? SCPQP_GROUP : 1;
     lint* flag = (lint*)(L.red + 120);   // [step parity]
-    ldouble* dbuf = L.red + 64;          // pivots [step mod 4][CB]; a pair's slots are adjacent
+    ldouble* dbuf = L.red + 128;         // pivots [step mod 2G][CB]; a group's slots are adjacent
     PROF_T0();
     for (int r0 = 0, s = 0; r0 < n; r0 += CB, ++s) {
         const int par = s & 1;
         const int jb = min(CB, n - r0), r1 = r0 + jb;
-        // look-ahead source: the previous panel, or the previous pair on even paired steps
-        const int np = (PAIR && par == 0 && s >= 2) ? 2 : 1;
+        // look-ahead source: the panels factored since the last group update
+        const int sg = s % G;
+        const int np = G == 1 ? 1 : (sg == 0 ? G : sg);
         const int jp = r0 - np * CB;   // < 0 at the first step: no look-ahead
-        const ldouble* dprev = dbuf + ((s - np) & 3) * CB;
+        const ldouble* dprev = dbuf + ((s - np) % (2 * G)) * CB;
         if (is_lead(L.lead)) {
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
-            ldouble* dn = dbuf + (s & 3) * CB;
+            ldouble* dn = dbuf + (s % (2 * G)) * CB;
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
         } else if (jp >= 0 && r1 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
-            if constexpr (PAIR) {
-                if (np == 2)
-                    trailing_update_mfma<(LT::OCCV >= 3 ? 2 : 4), 2 * CB / 4>(L.H, n, jp, r1, dprev, tw,
+            if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
+                if (sg == 0)
+                    trailing_update_mfma<(LT::OCCV >= 3 ? 2 : 4), G * CB / 4>(L.H, n, jp, r1, dprev, tw,
                                                                                NWAVE - 1);
-            } else if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
-                trailing_update_mfma<(LT::OCCV >= 3 ? 16 : 32) / CB, CB / 4>(L.H, n, jp, r1, dprev, tw,
-                                                                           NWAVE - 1);
             } else {
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
             }
