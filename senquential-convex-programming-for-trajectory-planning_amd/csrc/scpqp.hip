@@ -1216,16 +1216,29 @@ typedef double double4v __attribute__((ext_vector_type(4)));
 // U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
 // budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
 // tools/gpu_ab_libs.sh.
+// part: 0 all tiles; 1 / 2 the tile columns left / right of the split that halves
+// the tile count (column tile 0, the next panels' columns, always in part 1).
+// Tiles are enumerated column by column, so each part is a contiguous range.
 template <int U, int KS, class HP>
 __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
-                                                     int wave, int nwave) {
+                                                     int wave, int nwave, int part = 0) {
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     double dk[KS];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) dk[kk] = dcur[4 * kk + lk];
     const int T = (n - r1 + 15) >> 4;
     const int ntile = T * (T + 1) / 2;
-    for (int t = wave; t < ntile; t += U * nwave) {
+    int tb = 0, te = ntile;
+    if (part != 0) {
+        int js = 1, cum = T;   // tiles in the tile columns < js
+        while (js < T && 2 * cum < ntile) {
+            cum += T - js;
+            ++js;
+        }
+        if (part == 1) te = cum;
+        else tb = cum;
+    }
+    for (int t = tb + wave; t < te; t += U * nwave) {
         double a[U][KS], b[U][KS];
         double4v acc[U];
         int oc[U][4];
@@ -1233,9 +1246,11 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int tu = t + u * nwave;
-            int I = 0, J = 0;
-            tri_decode(tu < ntile ? tu : t, I, J);
-            const bool live = tu < ntile;
+            const bool live = tu < te;
+            int I = 0, J = 0;   // column-major order: the reversed row-major decode, mirrored
+            tri_decode(ntile - 1 - (live ? tu : t), J, I);
+            I = T - 1 - I;
+            J = T - 1 - J;
             const int i0 = r1 + 16 * I, k0 = r1 + 16 * J;
             const int ia = min(i0 + lr, n - 1), kb = min(k0 + lr, n - 1);
             const int oa = roff(ia) + j0, ob = roff(kb) + j0;
@@ -1279,6 +1294,9 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
 #endif
 static_assert(SCPQP_GROUP == 1 || SCPQP_GROUP == 2 || SCPQP_GROUP == 4, "group of 1, 2 or 4 panels");
 static_assert(2 * SCPQP_GROUP * CB <= 64, "the pivot buffer holds 64 entries");
+#ifndef SCPQP_SPLIT
+#define SCPQP_SPLIT 1
+#endif
 
 template <class LT>
 __device__ bool cholesky(const LT& L) {
@@ -1302,12 +1320,22 @@ __device__ bool cholesky(const LT& L) {
             ldouble* dn = dbuf + (s % (2 * G)) * CB;
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
-        } else if (jp >= 0 && r1 < n) {
+        } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
-                if (sg == 0)
-                    trailing_update_mfma<(LT::OCCV >= 3 ? 2 : 4), G * CB / 4>(L.H, n, jp, r1, dprev, tw,
-                                                                               NWAVE - 1);
+                constexpr int U = LT::OCCV >= 3 ? 2 : 4;
+                if constexpr (G == 2 && SCPQP_SPLIT) {
+                    // the pair's update in two halves: the left tile columns (they hold
+                    // the next two panels) on the even step, the rest on the odd step,
+                    // so the odd step's panel chain runs beside the trailing update
+                    if (sg == 0)
+                        trailing_update_mfma<U, 2 * CB / 4>(L.H, n, jp, r1, dprev, tw, NWAVE - 1, 1);
+                    else if (s >= 3)
+                        trailing_update_mfma<U, 2 * CB / 4>(L.H, n, r0 - 3 * CB, r0, dbuf + ((s - 3) & 3) * CB,
+                                                            tw, NWAVE - 1, 2);
+                } else if (sg == 0) {
+                    trailing_update_mfma<U, G * CB / 4>(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
+                }
             } else {
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
             }
