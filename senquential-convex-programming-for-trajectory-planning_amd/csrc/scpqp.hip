@@ -889,6 +889,87 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
 // ---------------------------------------------------------------------------
 // Normal matrix assembly  K = P_s + rho I + G' diag(d) G   (lower triangle)
 // ---------------------------------------------------------------------------
+// K_uu lower triangle in TS x TS tiles (rows l0 .. l0+TS-1 of vehicle a x columns
+// m0 .. m0+TS-1 of vehicle b, a >= b): K_(a,l),(b,l') = sum_k g_a,k-l' W~_ab,k
+// g_b,k-l' over k >= max(l, l').  Per k one W~ block and TS g 2-vectors of each
+// vehicle serve TS^2 entries; the g operands slide (row l0+i at step k uses the
+// value row l0+i-1 used at step k-1), so a step loads one new g of each vehicle
+// and one W~ block.  g indices below 0 read as zero, which gives each entry its
+// own lower summation bound.  A tile's cost is its trip count Hb - TS max(lt, mt):
+// tiles are enumerated by decreasing cost and dealt to the threads in snake
+// order, so every thread gets about the same number of trips.
+template <int TS, class LT, class PD>
+__device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD d, double rho) {
+    const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb, N = L.N;
+    const double u2 = P.uLim * P.uLim;
+    const int TH = (Hb + TS - 1) / TS, TD = TH * (TH + 1) / 2, TO = TH * TH;
+    const int PV = V * (V - 1) / 2;
+    const int ntile = V * TD + PV * TO;
+    const double2v zero2 = {0.0, 0.0};
+    for (int r0 = 0; r0 < ntile; r0 += NT) {
+        const int t = r0 + (((r0 / NT) & 1) ? NT - 1 - tid : tid);
+        if (t >= ntile) continue;
+        int a_, b_, lt, mt;
+        tile_decode(t, V, PV, a_, b_, lt, mt);
+        const int l0 = TS * lt, m0 = TS * mt, k0 = l0 > m0 ? l0 : m0;
+        const ldouble* ga = L.g + a_ * Hb * 2;
+        const ldouble* gb = L.g + b_ * Hb * 2;
+        const auto* W = L.Wt + 4 * (a_ * (a_ + 1) / 2 + b_);
+        double2v av[TS], bv[TS];   // the window at step k0 - 1
+#pragma unroll
+        for (int i = 0; i < TS; ++i) {
+            const int ia = k0 - 1 - l0 - i, ib = k0 - 1 - m0 - i;
+            av[i] = ia >= 0 ? ld2(ga + 2 * ia) : zero2;
+            bv[i] = ib >= 0 ? ld2(gb + 2 * ib) : zero2;
+        }
+        double c[TS][TS];
+#pragma unroll
+        for (int i = 0; i < TS; ++i)
+#pragma unroll
+            for (int j = 0; j < TS; ++j) c[i][j] = 0.0;
+        for (int k = k0; k < Hb; ++k) {
+            if constexpr (TS == 2) {
+                // 2 x 2 (c2): reloading the second row / column measured ~1 % faster
+                // than the sliding window (profiles/r02_ab_assembly.txt)
+                av[0] = ld2(ga + 2 * (k - l0));
+                bv[0] = ld2(gb + 2 * (k - m0));
+                av[1] = k > l0 ? ld2(ga + 2 * (k - l0 - 1)) : zero2;
+                bv[1] = k > m0 ? ld2(gb + 2 * (k - m0 - 1)) : zero2;
+            } else {
+#pragma unroll
+                for (int i = TS - 1; i > 0; --i) {
+                    av[i] = av[i - 1];
+                    bv[i] = bv[i - 1];
+                }
+                av[0] = ld2(ga + 2 * (k - l0));
+                bv[0] = ld2(gb + 2 * (k - m0));
+            }
+            const double2v w0 = ld2(W + 4 * k * nb), w1 = ld2(W + 4 * k * nb + 2);
+            double px[TS], py[TS];   // W~ g_b for every column
+#pragma unroll
+            for (int j = 0; j < TS; ++j) {
+                px[j] = w0.x * bv[j].x + w0.y * bv[j].y;
+                py[j] = w1.x * bv[j].x + w1.y * bv[j].y;
+            }
+#pragma unroll
+            for (int i = 0; i < TS; ++i)
+#pragma unroll
+                for (int j = 0; j < TS; ++j) c[i][j] += av[i].x * px[j] + av[i].y * py[j];
+        }
+#pragma unroll
+        for (int di = 0; di < TS; ++di)
+#pragma unroll
+            for (int dj = 0; dj < TS; ++dj) {
+                const int l = l0 + di, lp = m0 + dj;
+                if (l >= Hb || lp >= Hb || (a_ == b_ && lp > l)) continue;
+                const int row = a_ * Hb + l, col = b_ * Hb + lp;
+                double acc = c[di][dj];
+                if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
+                L.H[roff(row) + col] = acc;
+            }
+    }
+}
+
 template <class LT, class PD>
 __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb;
@@ -943,56 +1024,19 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
     double red[4] = {ww, 0.0, 0.0, 0.0};
     block_reduce4<1>(red, 0, L.red);
-    // phase 2: K_uu lower triangle in 2x2 tiles (rows l0, l0+1 of vehicle a x
-    // columns m0, m0+1 of vehicle b, a >= b): per k one W~ block and four g
-    // blocks serve four entries.  g indices below 0 read as zero, which gives
-    // each entry its own lower summation bound max(l, l').
-    // A tile's cost is its trip count Hb - 2 max(lt, mt): tiles are enumerated by
-    // decreasing cost and dealt to the threads in snake order, so every thread
-    // gets about the same number of trips (c2: at most 32 against 54 for the
-    // block-by-block enumeration).
-    const int N = L.N;
-    const int TH = (Hb + 1) >> 1, TD = TH * (TH + 1) / 2, TO = TH * TH;
-    const int PV = V * (V - 1) / 2;
-    const int ntile = V * TD + PV * TO;
-    for (int r0 = 0; r0 < ntile; r0 += NT) {
-        const int t = r0 + (((r0 / NT) & 1) ? NT - 1 - tid : tid);
-        if (t >= ntile) continue;
-        int a_, b_, lt, mt;
-        tile_decode(t, V, PV, a_, b_, lt, mt);
-        const int l0 = 2 * lt, m0 = 2 * mt;
-        const ldouble* ga = L.g + a_ * Hb * 2;
-        const ldouble* gb = L.g + b_ * Hb * 2;
-        const auto* W = L.Wt + 4 * (a_ * (a_ + 1) / 2 + b_);
-        double c00 = 0.0, c01 = 0.0, c10 = 0.0, c11 = 0.0;
-        for (int k = l0 > m0 ? l0 : m0; k < Hb; ++k) {
-            const double2v a0 = ld2(ga + (k - l0) * 2);
-            const double2v b0 = ld2(gb + (k - m0) * 2);
-            double2v a1 = ld2(ga + (k - l0 - 1) * 2), b1 = ld2(gb + (k - m0 - 1) * 2);
-            if (k == l0) a1 = double2v{0.0, 0.0};
-            if (k == m0) b1 = double2v{0.0, 0.0};
-            const double2v w0 = ld2(W + 4 * k * nb), w1 = ld2(W + 4 * k * nb + 2);
-            // W g_b for both columns
-            const double p0x = w0.x * b0.x + w0.y * b0.y, p0y = w1.x * b0.x + w1.y * b0.y;
-            const double p1x = w0.x * b1.x + w0.y * b1.y, p1y = w1.x * b1.x + w1.y * b1.y;
-            c00 += a0.x * p0x + a0.y * p0y;
-            c01 += a0.x * p1x + a0.y * p1y;
-            c10 += a1.x * p0x + a1.y * p0y;
-            c11 += a1.x * p1x + a1.y * p1y;
-        }
-        const double cc[2][2] = {{c00, c01}, {c10, c11}};
-#pragma unroll
-        for (int di = 0; di < 2; ++di)
-#pragma unroll
-            for (int dj = 0; dj < 2; ++dj) {
-                const int l = l0 + di, lp = m0 + dj;
-                if (l >= Hb || lp >= Hb || (a_ == b_ && lp > l)) continue;
-                const int row = a_ * Hb + l, col = b_ * Hb + lp;
-                double acc = cc[di][dj];
-                if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
-                L.H[roff(row) + col] = acc;
-            }
+    // phase 2: K_uu lower triangle in TS x TS tiles (assemble_tiles); 4 x 4 where
+    // there are enough of them to give every thread two (only the workspace plans
+    // have such horizons: the LDS-plan kernels do not carry the 4 x 4 registers)
+    const int T4 = (Hb + 3) >> 2, PV = V * (V - 1) / 2;
+    if constexpr (LT::HGLOBAL) {
+        if (V * (T4 * (T4 + 1) / 2) + PV * T4 * T4 >= 2 * NT) assemble_tiles<4>(P, L, d, rho);
+        else assemble_tiles<2>(P, L, d, rho);
+    } else {
+        (void)T4;
+        (void)PV;
+        assemble_tiles<2>(P, L, d, rho);
     }
+    const int N = L.N;
     toeplitz_t_apply(L, L.yb, [&](int e, double tt) { L.H[roff(N) + e] = tt; });
     if (tid == 0) L.H[roff(N) + N] = red[0] + d[L.mc - 1] + rho;
     __syncthreads();
@@ -1367,12 +1411,14 @@ __device__ bool cholesky(const LT& L) {
 // are faster in isolation but slower inside the kernel, the third is slower.)
 // ---------------------------------------------------------------------------
 
-template <int R, class HP>
-struct Solver {
 #ifndef SCPQP_SCH
-#define SCPQP_SCH 4
+#define SCPQP_SCH 4     // chunk of a factor in LDS
 #endif
-    static constexpr int SCH = SCPQP_SCH;   // chunk (columns / rows) streamed per step group
+#ifndef SCPQP_SCH_G
+#define SCPQP_SCH_G 8   // chunk of a factor in the workspace: twice the steps cover the L2 latency
+#endif
+template <int R, class HP, int SCH>
+struct Solver {   // SCH: chunk (columns / rows) streamed per step group
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
     int lane, n, ld;
@@ -1491,7 +1537,7 @@ struct Solver {
 
 template <int R, class LT>
 __device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, ldouble* x) {
-    Solver<R, decltype(L.H)> S(L.H, L.dinv, L.n, L.ld, bvec);
+    Solver<R, decltype(L.H), (LT::HGLOBAL ? SCPQP_SCH_G : SCPQP_SCH)> S(L.H, L.dinv, L.n, L.ld, bvec);
     S.run(x);
 }
 

@@ -17,7 +17,10 @@ names = ["ipm-loop-top", "residuals(first)", "scale+assemble+rhs", "cholesky", "
          "chol:panel0", "chol:steps", "solve:fwd", "solve:bwd",   # 12-15: sub-phases of 3 / 9
          "ipm-init", "take_u+evaluate",
          "panel:load", "panel:lookahead", "panel:pivots", "panel:store", "barrier-wait(w0)", "barrier-wait(w1)"]
-for nv, hp, B in [(4, 20, 1), (4, 20, 1024), (8, 30, 1)]:
+CFGS = [(4, 20, 1), (4, 20, 1024), (8, 30, 1)]
+if len(sys.argv) > 1:   # e.g. 8:30:1024
+    CFGS = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]]
+for nv, hp, B in CFGS:
     sc = R.circle_scenario(nv, Hp=hp)
     bt = BT.make_batch(sc, B, base_seed=1000)
     S = ScpQpSolver(sc, max_batch=B)
