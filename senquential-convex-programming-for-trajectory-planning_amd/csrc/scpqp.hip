@@ -1367,7 +1367,10 @@ __device__ bool cholesky(const LT& L) {
         } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
-                constexpr int U = LT::OCCV >= 3 ? 2 : 4;
+#ifndef SCPQP_TRAIL_U2
+#define SCPQP_TRAIL_U2 4
+#endif
+                constexpr int U = LT::OCCV >= 3 ? 2 : SCPQP_TRAIL_U2;   // tiles in flight per wave
                 if constexpr (G == 2 && SCPQP_SPLIT) {
                     // the pair's update in two halves: the left tile columns (they hold
                     // the next two panels) on the even step, the rest on the odd step,
@@ -2059,7 +2062,8 @@ PHASE D4 ph_polish_dual_next(Ctx c, int ref, int cap, double early) {
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
 // Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
 // violated inactive rows, drop the active rows with negative multipliers, and
-// rebuild the polish weights.  Returns 1 accepted, 2 corrected (retry), 0 stuck.
+// rebuild the polish weights.  Returns 1 accepted, 1 + (rows changed) >= 2
+// corrected (retry), 0 stuck.
 PHASE int ph_polish_accept(Ctx c, double hmax, int converged) {
     LAYDEF;
     const int tid = threadIdx.x;
@@ -2092,15 +2096,15 @@ PHASE int ph_polish_accept(Ctx c, double hmax, int converged) {
         const bool add = !act && L.rp[r] > vtol;
         const bool drop = act && L.la[r] < ytol;
         if (add || drop) {
-            changed = 1.0;
+            changed += 1.0;
             L.sa[r] = add ? 1.0 : 0.0;
             L.la[r] = 0.0;
             L.dd[r] = add ? idl : 0.0;
         }
     }
     double red2[4] = {changed, 0.0, 0.0, 0.0};
-    block_reduce4<1>(red2, 1, L.red);
-    return red2[0] != 0.0 ? 2 : 0;
+    block_reduce4<1>(red2, 0, L.red);
+    return red2[0] != 0.0 ? 1 + (int)red2[0] : 0;
 }
 // u-bar <- uLim * z  (unscaled controls of the QP solution)
 PHASE void ph_take_u(Ctx c) {
@@ -2149,6 +2153,16 @@ constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: 
 // than this in scaled units): the correction comes earlier and the refinement
 // spent on a wrong active set is skipped.
 constexpr double kWarmEarly = 1e-6;
+// For the largest factors (plan 2 with 4 row slots: c3) a warm start whose
+// active-set corrections stop shrinking is abandoned for the cold IPM.  There
+// half the warm starts fail, each after all kWarmRounds refactorisations, and a
+// round costs as much as an IPM iteration; c2-size problems, whose late warm
+// rounds often still certify, keep all rounds (tools/warm_policy_study.py:
+// c3 sample -11 % of the warm-path cycles, c2 sample +37 %).
+#ifndef SCPQP_WARM_STALL
+#define SCPQP_WARM_STALL 1
+#endif
+constexpr bool kWarmStall = SCPQP_WARM_STALL;
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
@@ -2162,10 +2176,13 @@ struct QpStats {
 // refined until x stops moving (|dx| <= kPolishTol max(1, |x|), at most
 // P.nRefine solves per round), certified, else the active set is corrected
 // (primal-dual active set) and the round repeats.  Returns true if certified.
+// stall: give up once a correction changes no fewer rows than the one before
+// (warm rounds of the c3-class plan, see kWarmStall).
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, int max_rounds,
-                                              int cap, double early, QpStats& st) {
+                                              int cap, double early, QpStats& st, bool stall = false) {
     bool ok = false, refactor = true, extended = false;
+    int prev_chg = 1 << 30;
     PROF_T0();
     for (int round = 0; round < max_rounds && !ok; ++round) {
         ++st.rounds;
@@ -2188,12 +2205,16 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, in
         const int acc = PH(ph_polish_accept)(c, hmax, conv);
         PROF_ACC(8);
         ok = acc == 1;
-        // acc 2: active set corrected -> refactor;  acc 0 with the multiplier
+        // acc >= 2: active set corrected -> refactor;  acc 0 with the multiplier
         // iteration still moving: same active set, keep iterating on the same
         // factor;  acc 0 after convergence: stuck, give up
         if (acc == 0 && (conv || extended)) break;
+        if (acc >= 2) {
+            if (stall && round >= 1 && acc - 1 >= prev_chg) break;
+            prev_chg = acc - 1;
+        }
         extended |= acc == 0;   // one extra batch of iterations per QP
-        refactor = acc == 2;
+        refactor = acc >= 2;
     }
     return ok;
 }
@@ -2218,7 +2239,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     if (warm) {
         PH(ph_polish_warm)(c);
         if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, kWarmRounds, kWarmRefine, kWarmEarly,
-                                           st)) {
+                                           st, kWarmStall && HG && VG && RM == 4)) {
             ++st.warm_ok;
             return true;
         }
