@@ -1783,6 +1783,14 @@ struct D4 {
 // set is wrong (warm rounds: a violated inactive row or a negative active
 // multiplier beyond `early`), 0 to continue.  Never before the second solve.
 constexpr double kPolishTol = 1e-10;
+// The polish penalty of a warm start (the previous QP's active set) is
+// kWarmDeltaScale x polish_delta; the cold polish after the IPM uses polish_delta.
+// 1/delta of the current round lives in red[kIdlSlot] (set by the prep phases).
+#ifndef SCPQP_WARM_DSCALE
+#define SCPQP_WARM_DSCALE 1.0
+#endif
+constexpr double kWarmDeltaScale = SCPQP_WARM_DSCALE;
+constexpr int kIdlSlot = 122;
 __device__ __forceinline__ int polish_stop(const D4& d, int ref, double early) {
     if (ref < 1) return 0;
     if (d.a <= kPolishTol * fmax(1.0, d.b)) return 1;
@@ -1981,6 +1989,7 @@ PHASE D4 ph_back_update_residuals(Ctx c, double smu) {
 PHASE void ph_polish_prep(Ctx c) {
     LAYDEF;
     const double idl = 1.0 / P.polDelta;
+    if (threadIdx.x == 0) L.red[kIdlSlot] = idl;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const bool act = L.lam[r] > L.s[r];
         L.dd[r] = act ? idl : 0.0;
@@ -1994,7 +2003,8 @@ PHASE void ph_polish_prep(Ctx c) {
 // multipliers (la) on the re-linearised rows, x_0 = its solution (z)
 PHASE void ph_polish_warm(Ctx c) {
     LAYDEF;
-    const double idl = 1.0 / P.polDelta;
+    const double idl = 1.0 / (kWarmDeltaScale * P.polDelta);
+    if (threadIdx.x == 0) L.red[kIdlSlot] = idl;
     for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.sa[r] != 0.0 ? idl : 0.0;
     for (int e = threadIdx.x; e < L.n; e += NT) L.dz[e] = L.rd[e] = L.z[e];
     __syncthreads();
@@ -2014,7 +2024,7 @@ PHASE D4 ph_scales(Ctx c) {
 // polish right-hand side: tv = mask (h / delta - y), rhs = -q + G' tv + rho x_k
 template <class LT>
 __device__ __forceinline__ void polish_rhs_body(const cParams& P, const LT& L) {
-    const double idl = 1.0 / P.polDelta;
+    const double idl = L.red[kIdlSlot];
     for (int r = threadIdx.x; r < L.mc; r += NT) L.tv[r] = L.sa[r] * (hval(L, r) * idl - L.la[r]);
     __syncthreads();
     rhs_from_tv_body(P, L, P.polRho);
@@ -2028,7 +2038,7 @@ PHASE void ph_polish_rhs(Ctx c) {
 // the active rows} (x_{k-1} kept in rd, dead during the polish).
 template <class LT>
 __device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
-    const double idl = 1.0 / P.polDelta;
+    const double idl = L.red[kIdlSlot];
     g_apply(L, L.dz, L.rp, true);
     double viol = -1e300, yneg = -1e300;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
@@ -2089,7 +2099,7 @@ PHASE int ph_polish_accept(Ctx c, double hmax, int converged) {
         return 1;
     }
     if (red[3] != 0.0) return 0;
-    const double idl = 1.0 / P.polDelta;
+    const double idl = L.red[kIdlSlot];
     double changed = 0.0;
     for (int r = tid; r < L.mc; r += NT) {
         const bool act = L.sa[r] != 0.0;
@@ -2163,6 +2173,17 @@ constexpr double kWarmEarly = 1e-6;
 #define SCPQP_WARM_STALL 1
 #endif
 constexpr bool kWarmStall = SCPQP_WARM_STALL;
+// Warm-round caps and early-correction threshold of the c3-class plan (A/B knobs;
+// the defaults are the c2 values above).
+#ifndef SCPQP_WARM_ROUNDS_WIDE
+#define SCPQP_WARM_ROUNDS_WIDE 8
+#endif
+#ifndef SCPQP_WARM_REFINE_WIDE
+#define SCPQP_WARM_REFINE_WIDE 12
+#endif
+#ifndef SCPQP_WARM_EARLY_WIDE
+#define SCPQP_WARM_EARLY_WIDE 1e-6
+#endif
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
@@ -2238,8 +2259,11 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     const double hmax = sc.a, qmax = sc.b;
     if (warm) {
         PH(ph_polish_warm)(c);
-        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, kWarmRounds, kWarmRefine, kWarmEarly,
-                                           st, kWarmStall && HG && VG && RM == 4)) {
+        constexpr bool wide = HG && VG && RM == 4;
+        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, wide ? SCPQP_WARM_ROUNDS_WIDE : kWarmRounds,
+                                           wide ? SCPQP_WARM_REFINE_WIDE : kWarmRefine,
+                                           wide ? SCPQP_WARM_EARLY_WIDE : kWarmEarly, st,
+                                           kWarmStall && wide)) {
             ++st.warm_ok;
             return true;
         }
@@ -2710,7 +2734,7 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
     P.maxPts = p->ref_max_pts > 0 ? p->ref_max_pts : 2;
     P.maxScp = p->max_scp_iter > 0 ? p->max_scp_iter : 20;
     P.maxIpm = p->max_ipm_iter > 0 ? p->max_ipm_iter : 60;
-    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 40;
+    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 12;
     P.flags = p->flags;
     P.dt = p->dt;
     P.uLim = p->u_lim;

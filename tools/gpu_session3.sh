@@ -1,0 +1,23 @@
+#!/bin/bash
+# Shipped-library session: full GPU test suite, the polish-cap parity check on c3
+# (converged problems, cap 40 vs 12), then the c2 and c3 bench lines with their CPU legs.
+#   gpurun --timeout 1200 -- bash tools/gpu_session3.sh <tag>
+set -u
+TAG=${1:-s3}; OUT=gpurun_out/$TAG; mkdir -p $OUT gpurun_out/pab
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> cmd...
+    local name=$1 secs=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    if [ $rc -ne 0 ]; then grep -B30 "^E " "$OUT/$name.log" | tail -60; tail -n 20 "$OUT/$name.log"; echo "!! $name rc=$rc"; exit $rc; fi
+}
+step pytest 900 python -u -m pytest tests -m gpu -v -x -p no:cacheprovider --timeout 300 --timeout-method thread
+grep -E "passed|failed" $OUT/pytest.log | tail -2
+step cap_c3 300 python -u tools/gpu_param_ab.py c3:1 polish_refine=40 polish_refine=12
+step cap_c2 300 python -u tools/gpu_param_ab.py c2:5 polish_refine=40 polish_refine=12
+step bench_c2 400 python bench.py
+grep '^{' $OUT/bench_c2.log > $OUT/bench_c2.json
+step bench_c3 600 python bench.py --config c3 --steps 3 --warmup 1
+grep '^{' $OUT/bench_c3.log > $OUT/bench_c3.json
+echo "== done $(date +%T)"
