@@ -20,4 +20,11 @@ step bench_c2 400 python bench.py
 grep '^{' $OUT/bench_c2.log > $OUT/bench_c2.json
 step bench_c3 600 python bench.py --config c3 --steps 3 --warmup 1
 grep '^{' $OUT/bench_c3.log > $OUT/bench_c3.json
+
+# optional: A/B of library variants under ab/ against the shipped library
+if ls ab/*.so > /dev/null 2>&1; then
+    ln -sf ../senquential-convex-programming-for-trajectory-planning_amd/scpqp/libscpqp.so ab/shipped.so
+    bash tools/gpu_ab_cfgs.sh ${TAG}_ab "c2:20 c3:2" "" ab/shipped.so ab/*[^d].so > $OUT/ab.txt 2>&1
+    cat $OUT/ab.txt
+fi
 echo "== done $(date +%T)"
