@@ -692,7 +692,7 @@ IPM_TOL = 1e-10
 POLISH_DELTA = 3e-7
 POLISH_RHO = 1e-12
 POLISH_REFINE = 12          # cap on multiplier-iteration solves per polish round (HIP default; 40 for n > 192)
-POLISH_TOL = 1e-10          # the iteration stops once max|x_k - x_{k-1}| <= tol max(1, |x_k|)
+POLISH_TOL = 1e-9           # the iteration stops once max|x_k - x_{k-1}| <= tol max(1, |x_k|)
 
 
 @dataclass

@@ -1782,7 +1782,10 @@ struct D4 {
 // x stops moving (|dx| <= tol max(1, |x|)), 2 when the iterate shows the active
 // set is wrong (warm rounds: a violated inactive row or a negative active
 // multiplier beyond `early`), 0 to continue.  Never before the second solve.
-constexpr double kPolishTol = 1e-10;
+#ifndef SCPQP_POLISH_TOL
+#define SCPQP_POLISH_TOL 1e-9
+#endif
+constexpr double kPolishTol = SCPQP_POLISH_TOL;
 // The polish penalty of a warm start (the previous QP's active set) is
 // kWarmDeltaScale x polish_delta; the cold polish after the IPM uses polish_delta.
 // 1/delta of the current round lives in red[kIdlSlot] (set by the prep phases).

@@ -65,8 +65,13 @@ def main():
                     f"ipm/qp {out.n_ipm.cpu().numpy().sum() / nqp:.2f}  "
                     f"polish solves/qp {out.n_refine.cpu().numpy().sum() / nqp:.2f}  "
                     f"warm ok/qp {out.n_warm.cpu().numpy().sum() / nqp:.3f}  conv {np.mean((st & 0xff) == 0):.4f}  rej {np.mean((st & 0x100) != 0):.4f}")
+            if ref is None and os.environ.get("CMP"):   # first set of another library's run
+                z = np.load(os.environ["CMP"])
+                ref = (z["u"], z["nscp"], z["st"])
             if ref is None:
                 ref = (u, nscp, st)
+                if os.environ.get("SAVE"):
+                    np.savez(os.environ["SAVE"], u=u, nscp=nscp, st=st)
             else:
                 same = nscp == ref[1]
                 du = np.abs(u[same] - ref[0][same]).max() if same.any() else float("nan")
