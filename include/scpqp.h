@@ -74,7 +74,7 @@ typedef struct scpqp_params {
     double slack_weight;     /* 1e5  (SCP_controller.py:84)                            */
     int32_t max_scp_iter;    /* 20   (SCP_controller.py:86)                            */
     int32_t max_ipm_iter;    /* IPM iteration cap per QP (e.g. 60)                     */
-    int32_t polish_refine;   /* polish solve cap per round (0: 12, 40 if n > 192)   */
+    int32_t polish_refine;   /* cap on multiplier-iteration solves per round (0: 40) */
     int32_t flags;           /* SCPQP_FLAG_* (obstacle quirk B.4 on by default)        */
     double ipm_tol;          /* scaled KKT tolerance of the IPM (e.g. 1e-9)            */
     double polish_delta;     /* polish penalty delta (scaled units, default 3e-7)      */

@@ -691,7 +691,7 @@ def evaluate_structured(p: Problem, lin: Linearisation, u, tol=CONSTRAINT_TOL, o
 IPM_TOL = 1e-10
 POLISH_DELTA = 3e-7
 POLISH_RHO = 1e-12
-POLISH_REFINE = 12          # cap on multiplier-iteration solves per polish round (HIP default; 40 for n > 192)
+POLISH_REFINE = 40          # cap on multiplier-iteration solves per polish round
 POLISH_TOL = 1e-9           # the iteration stops once max|x_k - x_{k-1}| <= tol max(1, |x_k|)
 
 

@@ -2743,11 +2743,7 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
     P.maxPts = p->ref_max_pts > 0 ? p->ref_max_pts : 2;
     P.maxScp = p->max_scp_iter > 0 ? p->max_scp_iter : 20;
     P.maxIpm = p->max_ipm_iter > 0 ? p->max_ipm_iter : 60;
-    // default polish solve cap: 12, except for factors of more than 192 rows (c3
-    // class), which keep 40 -- at 12 there 38 % of the problems keep an IPM iterate
-    // for some QP and converged answers move by up to 6e-7 rad
-    const int rowSlots = (V * dims->hp_max + 1 + 63) / 64;
-    P.nRefine = p->polish_refine > 0 ? p->polish_refine : (rowSlots >= 4 ? 40 : 12);
+    P.nRefine = p->polish_refine > 0 ? p->polish_refine : 40;
     P.flags = p->flags;
     P.dt = p->dt;
     P.uLim = p->u_lim;
