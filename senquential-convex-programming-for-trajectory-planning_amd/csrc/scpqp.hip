@@ -2172,12 +2172,13 @@ constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: 
 // than this in scaled units): the correction comes earlier and the refinement
 // spent on a wrong active set is skipped.
 constexpr double kWarmEarly = 1e-6;
-// For the largest factors (plan 2 with 4 row slots: c3) a warm start whose
-// active-set corrections stop shrinking is abandoned for the cold IPM.  There
-// half the warm starts fail, each after all kWarmRounds refactorisations, and a
-// round costs as much as an IPM iteration; c2-size problems, whose late warm
-// rounds often still certify, keep all rounds (tools/warm_policy_study.py:
-// c3 sample -11 % of the warm-path cycles, c2 sample +37 %).
+// A warm start whose active-set corrections stop shrinking is abandoned for the
+// cold IPM.  On c3 half the warm starts fail, each after all kWarmRounds
+// refactorisations, and a round costs as much as an IPM iteration (c3 4.45k ->
+// 4.79k solves/s).  At the round-1 polish stopping tolerance the late warm rounds
+// of c2-size problems still certified often enough that the rule cost c2 1-2 %
+// (tools/warm_policy_study.py); with the 1e-9 tolerance it gains c2 2-3 %
+// (profiles/r02_ab_warm_stall.txt), so it applies to every plan.
 #ifndef SCPQP_WARM_STALL
 #define SCPQP_WARM_STALL 1
 #endif
@@ -2207,7 +2208,7 @@ struct QpStats {
 // P.nRefine solves per round), certified, else the active set is corrected
 // (primal-dual active set) and the round repeats.  Returns true if certified.
 // stall: give up once a correction changes no fewer rows than the one before
-// (warm rounds of the c3-class plan, see kWarmStall).
+// (warm rounds, see kWarmStall).
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, int max_rounds,
                                               int cap, double early, QpStats& st, bool stall = false) {
@@ -2272,7 +2273,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
         if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, wide ? SCPQP_WARM_ROUNDS_WIDE : kWarmRounds,
                                            wide ? SCPQP_WARM_REFINE_WIDE : kWarmRefine,
                                            wide ? SCPQP_WARM_EARLY_WIDE : kWarmEarly, st,
-                                           kWarmStall && wide)) {
+                                           kWarmStall)) {
             ++st.warm_ok;
             return true;
         }
