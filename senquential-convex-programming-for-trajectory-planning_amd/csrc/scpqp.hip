@@ -122,7 +122,7 @@ enum Mode { MODE_SOLVE = 0, MODE_LINEARIZE = 1, MODE_EVALUATE = 2, MODE_SAMPLE =
 
 struct KArgs {
     const DevParams* P;
-    int B, mode, maxScp, tail;   // tail: batch of <= 2 problems per resident workgroup
+    int B, mode, maxScp, pad0;
     const double *x0, *u0, *ec, *obst, *refIn, *uWarm, *uEval;
     const int* hp;
     double *uOut, *trajOut, *obj, *maxv, *sumv;
@@ -2175,11 +2175,10 @@ constexpr double kWarmEarly = 1e-6;
 // A warm start whose active-set corrections stop shrinking is abandoned for the
 // cold IPM.  On c3 half the warm starts fail, each after all kWarmRounds
 // refactorisations, and a round costs as much as an IPM iteration (c3 4.45k ->
-// 4.79k solves/s): the c3-class plan always takes the rule.  On c2-size problems
-// the late warm rounds still certify often, so the rule raises the mean cost per
-// problem (c4, 8 problems per workgroup: -5 %) but shortens the slowest problems
-// (c2, B = 1024 on 768 workgroups: +3-4 %); there it is taken only by tail-bound
-// launches (KArgs.tail, profiles/r02_ab_warm_stall.txt).
+// 4.79k solves/s).  At the round-1 polish stopping tolerance the late warm rounds
+// of c2-size problems still certified often enough that the rule cost c2 1-2 %
+// (tools/warm_policy_study.py); with the 1e-9 tolerance it gains c2 2-3 %
+// (profiles/r02_ab_warm_stall.txt), so it applies to every plan.
 #ifndef SCPQP_WARM_STALL
 #define SCPQP_WARM_STALL 1
 #endif
@@ -2264,7 +2263,7 @@ struct QpKnobs {
 };
 template <bool HG, bool VG, int RM, int OCC>
 __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qflags, bool warm,
-                                              bool tail, QpStats& st) {
+                                              QpStats& st) {
     const int mc = K.mc;
     const D4 sc = PH(ph_scales)(c);
     const double hmax = sc.a, qmax = sc.b;
@@ -2274,7 +2273,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
         if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, wide ? SCPQP_WARM_ROUNDS_WIDE : kWarmRounds,
                                            wide ? SCPQP_WARM_REFINE_WIDE : kWarmRefine,
                                            wide ? SCPQP_WARM_EARLY_WIDE : kWarmEarly, st,
-                                           kWarmStall && (wide || tail))) {
+                                           kWarmStall)) {
             ++st.warm_ok;
             return true;
         }
@@ -2324,7 +2323,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     return ok;
 }
 template <bool HG, bool VG, int RM, int OCC>
-__device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, bool tail, QpStats& st) {
+__device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, QpStats& st) {
     const Ctx c = uniform_ctx(c0);
     const cParams& P = *c.P;
     QpKnobs K;
@@ -2336,7 +2335,7 @@ __device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, bool tail,
     K.polRho = P.polRho;
     QpStats ls{0, 0, 0, 0};
     int lf = 0;
-    const bool ok = qp_solve_body<HG, VG, RM, OCC>(c, K, lf, warm, tail, ls);
+    const bool ok = qp_solve_body<HG, VG, RM, OCC>(c, K, lf, warm, ls);
     st.ipm += ls.ipm;
     st.rounds += ls.rounds;
     st.refine += ls.refine;
@@ -2488,7 +2487,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             // active-set corrections to recover it (tools/polish_study.py: 0/16)
             const int ipm_before = qs.ipm;
             const bool warm_qp = warm_on && prev_ok && it >= 2;
-            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_qp, a.tail != 0, qs);
+            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_qp, qs);
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
@@ -2658,9 +2657,6 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.ws = h->ws;
     a.wsStride = h->wsStride;
     a.counter = h->counter;
-    // tail-bound batch (at most two problems per resident workgroup): the makespan is
-    // the slowest problems', so warm starts take the stall rule (kWarmStall) on every plan
-    a.tail = a.B <= 2 * h->grid ? 1 : 0;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
     const int occ = h->occ;   // workgroups per CU the register budget is compiled for
