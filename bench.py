@@ -13,6 +13,10 @@ path ("weak" scaling); only a barrier and a max-reduction of the time.
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \\
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
 
+Without a launcher (no WORLD_SIZE in the environment), ``--gpus N`` with N > 1
+starts the N rank processes itself, one per GPU, before anything touches a GPU
+(spawn_ranks), and exits with the worst rank's return code.
+
 Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant (only)
 kernel against the FP64 peak with the algorithmic FLOP count of the executed
 algorithm (scpqp/flops.py); ``cpu_baseline`` times the in-repo CPU
@@ -91,6 +95,43 @@ def host_cores():
     return max(1, min(n, int(os.environ.get("SCPQP_CPU_WORKERS", "16"))))
 
 
+# ----------------------------------------------------------------------------- ranks
+def spawn_ranks(n):
+    """``bench.py --gpus N`` run directly: start the N ranks as child processes of
+    this one (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank r on GPU r) and
+    wait for them.  Nothing here initialises the GPU (device_count() does not on
+    this ROCm build).  More ranks than devices is a single-box rehearsal of the
+    sharded path: the ranks share devices and the collectives run on gloo (RCCL
+    refuses two ranks on one device).  If a rank fails, the others are stopped."""
+    import socket
+    import subprocess
+    import torch
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n))
+    ndev = torch.cuda.device_count()
+    if ndev < n:
+        print(f"bench: {n} ranks on {ndev} device(s): ranks share devices, gloo collectives",
+              file=sys.stderr, flush=True)
+        env0.setdefault("SCPQP_DIST_BACKEND", "gloo")
+    procs = [subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                              env=dict(env0, RANK=str(r), LOCAL_RANK=str(r))) for r in range(n)]
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or (code if code > 0 else 1)
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
 # ----------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -119,6 +160,8 @@ def main():
         args.n_veh, args.hp, args.batch = 4, 30, args.batch if args.batch != 1024 else 3072
         mixed = (10, 20, 30)
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -111,6 +111,62 @@ def plant_step_exact(sc, v, x_start, t0, u_of_k):
     return out
 
 
+# ---------------------------------------------------------------------------
+# The device's integrator restated (csrc/plant.hip): classical RK4 with equal steps of
+# at most H_MAX over each span.  Used by ClosedLoop(plant="rk4") to run the restated
+# closed loop on the device's plant arithmetic instead of the reference's scipy calls,
+# so that a divergence between the device loop and the restated loop can be pinned on
+# the integrator (dopri5 / LSODA vs RK4, ~1e-12 m) rather than on the solver.
+# ---------------------------------------------------------------------------
+H_MAX = 2.5e-3            # scpqp/plant.py H_MAX (a quarter tick)
+
+
+def _rk4_steps(T, hmax=H_MAX):
+    """plant.hip steps_for: ceil(|T| / hmax - 1e-9), at least 1."""
+    return max(1, int(math.ceil(abs(T) / hmax - 1e-9)))
+
+
+def _rk4_flow(x, T, u_ref, Lf, Lr, n):
+    """plant.hip flow(): n RK4 steps of h = T / n from x (Model.py:61-87 right-hand side)."""
+    x = np.array(x, float)
+    h = T / n
+    for _ in range(n):
+        k1 = R.bicycle_rhs(x, u_ref, Lf, Lr)
+        k2 = R.bicycle_rhs(x + 0.5 * h * k1, u_ref, Lf, Lr)
+        k3 = R.bicycle_rhs(x + 0.5 * h * k2, u_ref, Lf, Lr)
+        k4 = R.bicycle_rhs(x + h * k3, u_ref, Lf, Lr)
+        x = x + h / 6.0 * (k1 + 2.0 * k2 + 2.0 * k3 + k4)
+    return x
+
+
+def delay_compensate_rk4(sc, x_measured, u_hold, steps=DELAY_STEPS):
+    """delay_compensate on the device's integrator (plant.hip delay_kernel): the
+    outputs linspace(0, horizon, steps), each span integrated from the previous output."""
+    nV = len(u_hold)
+    span = delay_horizon(sc) / (steps - 1)
+    n = _rk4_steps(span)
+    traj = np.zeros((steps, NX, nV))
+    for v in range(nV):
+        x = np.asarray(x_measured[v], float)
+        traj[0, :, v] = x
+        for j in range(1, steps):
+            x = _rk4_flow(x, span, float(u_hold[v]), sc.Lf[v], sc.Lr[v], n)
+            traj[j, :, v] = x
+    return traj[-1].T.copy(), np.asarray(u_hold, float).copy(), traj
+
+
+def plant_step_rk4(sc, v, x_start, t0, u_of_k):
+    """plant_step on the device's integrator (plant.hip plant_kernel): output k
+    integrates k ticks from x_start with the control of tick k."""
+    K = sc.ticks_per_sim + 1
+    out = np.zeros((K, NX))
+    out[0] = x_start
+    for k in range(1, K):
+        T = k * sc.tick_length
+        out[k] = _rk4_flow(x_start, T, float(u_of_k[k]), sc.Lf[v], sc.Lr[v], _rk4_steps(T))
+    return out
+
+
 def clip_controls(U, u0, umax, du_lim):
     """main.py:164-174 on U [Hp, nVeh] (a copy is returned)."""
     U = np.array(U, float, copy=True)
@@ -190,8 +246,11 @@ class ClosedLoop:
     realisation with the SCP controller of ``scp_reference`` (structured mode).
     ``x_init`` [nVeh, 6] replaces scenario.x0 (main.py:73-75)."""
 
-    def __init__(self, sc, x_init=None):
+    def __init__(self, sc, x_init=None, plant="scipy"):
+        """``plant``: "scipy" — the reference's own integrator calls (odeint, dopri5);
+        "rk4" — the device's fixed-step RK4 restated (delay_compensate_rk4, plant_step_rk4)."""
         self.sc = sc
+        self.plant = plant
         nV = sc.nVeh
         self.du_lim = sc.mechanicalSteeringLimit * 2              # Scenarios.py:50
         self.path = np.full((NX, nV, sc.ticks_total + 1), np.nan)
@@ -215,7 +274,8 @@ class ClosedLoop:
         u_path = np.zeros((nV, n_path))
         lo = max(sc.ticks_delay_x - tick_now, 0)
         u_path[:, lo:lo + tick_act - 1 - tick_meas] = self.control[:, tick_meas + 1:tick_act]
-        x0, u0, dtraj = delay_compensate(sc, x_meas, u_path[:, -1])
+        dc = delay_compensate_rk4 if self.plant == "rk4" else delay_compensate
+        x0, u0, dtraj = dc(sc, x_meas, u_path[:, -1])
         obst = obstacle_prediction(sc, tick_meas)
         p = R.make_problem(sc, x0, u0, np.zeros((nV, 2)), Hp=sc.Hp, obst=obst)
         res = R.scp_solve(p, u_warm=self.u_prev, mode="structured")
@@ -227,7 +287,8 @@ class ClosedLoop:
             self.control[v, sl] = U[0, v]
             timelist = np.linspace(i * sc.dt, (i + 1) * sc.dt, tps + 1)
             u_of_k = [self.control[v, control_tick_index(sc, t)] for t in timelist]
-            ms = plant_step(sc, v, self.path[:, v, tick_now], i * sc.dt, u_of_k)
+            ps = plant_step_rk4 if self.plant == "rk4" else plant_step
+            ms = ps(sc, v, self.path[:, v, tick_now], i * sc.dt, u_of_k)
             self.path[:, v, tps * i + 1:tps * (i + 1) + 1] = ms[1:].T
         ev = evaluate_in_original_problem(sc, U, res.traj, p.ref_points,
                                           obst if sc.nObst else None)

@@ -17,8 +17,11 @@ What differs from the reference, on purpose:
   (SCP_controller.py:169-189: 'Aineq', 'bineq', 'x', 'slack', 'QCQP_ObjVal',
   'SCP_ObjVal', 'delta', 'u', 'prev_u', 'feasible'), rebuilt from the kernel's
   per-iteration trace, plus per-solve counters (SCP/IPM iterations, status
-  flags).  'P', 'q', 'lb', 'ub' are the same every iteration and are not
-  repeated; the forward_U trajectories of the log are not rebuilt;
+  flags).  The lists are decoded on first access (``_LazyLog``): main.py never
+  reads the log, so the device-to-host copy of the trace and the dense row
+  rebuild stay out of ``optimizerTime``.  'P', 'q', 'lb', 'ub' are the same
+  every iteration and are not repeated; the forward_U trajectories of the log
+  are not rebuilt;
 * the dense ``qcqp`` dictionary (QCQP_formulate, SCP_controller.py:278-341) is
   built lazily, only if a caller reads ``.qcqp``; the solve uses the
   factored forms on the device.
@@ -36,6 +39,53 @@ from MPC_Iter import MPCclass
 cfg = Config()
 
 ST_INVALID = 2      # SCPQP_ST_INVALID
+
+
+class _LazyLog(dict):
+    """optimization_log whose per-iteration lists are decoded from the device trace
+    the first time any key beyond the counters is read (or the log is iterated)."""
+
+    def __init__(self, counters, decode):
+        super().__init__(counters)
+        self._decode = decode
+
+    def _fill(self):
+        if self._decode is not None:
+            dec, self._decode = self._decode, None
+            super().update(dec())
+
+    def __getitem__(self, k):
+        if not super().__contains__(k):
+            self._fill()
+        return super().__getitem__(k)
+
+    def __contains__(self, k):
+        self._fill()
+        return super().__contains__(k)
+
+    def get(self, k, default=None):
+        self._fill()
+        return super().get(k, default)
+
+    def __iter__(self):
+        self._fill()
+        return super().__iter__()
+
+    def __len__(self):
+        self._fill()
+        return super().__len__()
+
+    def keys(self):
+        self._fill()
+        return super().keys()
+
+    def items(self):
+        self._fill()
+        return super().items()
+
+    def values(self):
+        self._fill()
+        return super().values()
 
 
 class SCPcontroller:
@@ -93,12 +143,12 @@ class SCPcontroller:
                                 **self._inputs())
         u = res.u[0, :self.nVeh * self.Hp].cpu().numpy().reshape(-1, 1)
         status = int(res.status[0].item())
-        log = {'status': status & 0xff, 'flags': status & ~0xff,
-               'n_scp': int(res.n_scp[0].item()), 'n_ipm': int(res.n_ipm[0].item()),
-               'obj': float(res.obj[0].item()),
-               'max_violation': float(res.max_violation[0].item()),
-               'sum_violations': float(res.sum_violations[0].item())}
-        log.update(self._iteration_log(res))
+        log = _LazyLog({'status': status & 0xff, 'flags': status & ~0xff,
+                        'n_scp': int(res.n_scp[0].item()), 'n_ipm': int(res.n_ipm[0].item()),
+                        'obj': float(res.obj[0].item()),
+                        'max_violation': float(res.max_violation[0].item()),
+                        'sum_violations': float(res.sum_violations[0].item())},
+                       lambda: self._iteration_log(res))
         self._last_traj = res.traj[0, :self.Hp].cpu().numpy()
         return u, bool(res.feasible[0].item()), float(res.obj[0].item()), log
 

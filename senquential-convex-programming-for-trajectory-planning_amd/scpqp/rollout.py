@@ -219,7 +219,13 @@ class ClosedLoopBatch:
         if self.trace:
             rec["u_warm"] = u_warm
             rec["obst"] = obst
-            rec["trace"] = out.trace.clone()
+            # kept on the host (a diagnostic mode: c2 at B = 1024 would hold ~106 MB per
+            # step on the device), up to the largest SCP count of the step; iterations
+            # past a problem's own n_scp stay NaN as on the device
+            ns = int(out.n_scp.max().item())
+            tr = torch.full((B,) + tuple(out.trace.shape[1:]), float("nan"), dtype=out.trace.dtype)
+            tr[:, :ns] = out.trace[:, :ns].cpu()
+            rec["trace"] = tr
             rec["u"] = out.u.clone()
         if self.timing:
             torch.cuda.synchronize(self.device)

@@ -15,6 +15,12 @@ Two comparisons per realisation and MPC step:
    device run are reported; they stay at integration-tolerance level as long as
    both loops take the same SCP iteration counts, and a stop flip (a threshold
    straddle, explained in 1.) legitimately moves the two loops apart afterwards.
+3. **Independent closed loop on the device's integrator** (``rk4_loop``): the
+   same restated loop with the reference's scipy integrator calls replaced by
+   the restated fixed-step RK4 of csrc/plant.hip (oracle/plant_reference.py
+   ``plant="rk4"``).  Where loop 2 parts from the device loop only because the
+   two integrators differ by ~1e-12 m (the noise-free circle's mirror-symmetric
+   bifurcation), loop 3 keeps following the device loop.
 
 Used by tests/test_gpu_closed_loop.py and tools/closed_loop_parity.py (which
 writes the profiles/ record).  The oracle runs in a spawned process pool, one
@@ -101,7 +107,8 @@ def run_device(case, B, steps, device):
 
 def check_realisation(args):
     """Oracle work for one realisation (runs in a worker).  Returns per-step metrics."""
-    case, x_init, recs, mirror_steps = args
+    case, x_init, recs, mirror_steps = args[:4]
+    rk4_loop = len(args) > 4 and args[4]
     _paths()
     from oracle import plant_reference as PR
     from oracle import scp_reference as R
@@ -110,8 +117,10 @@ def check_realisation(args):
     sc = scenario(case)
     nV, nO, Hp, tps = sc.nVeh, sc.nObst, sc.Hp, sc.ticks_per_sim
     ref = PR.ClosedLoop(sc, x_init=x_init)
+    ref4 = PR.ClosedLoop(sc, x_init=x_init, plant="rk4") if rk4_loop else None
     steps = []
     same_counts = True
+    same_counts4 = True
     for i, d in enumerate(recs):
         m = dict(step=i, n_scp_dev=d["n_scp"])
         # 1a. solve parity on the device's inputs
@@ -155,14 +164,27 @@ def check_realisation(args):
         m["loop_U_diff"] = float(np.max(np.abs(rr["U"] - d["U"])))
         want = ref.path[:, :, i * tps:(i + 1) * tps + 1].transpose(1, 2, 0)
         m["loop_path_diff"] = float(np.max(np.abs(want - d["path"])))
+        # 3. the independent restated loop on the device's integrator
+        if ref4 is not None:
+            r4 = ref4.step(i)
+            mir4 = (np.max(np.abs(r4["U"] + d["U"])) < np.max(np.abs(r4["U"] - d["U"]))
+                    and np.max(np.abs(r4["U"] - d["U"])) > 1e-4)
+            same_counts4 = same_counts4 and r4["n_scp"] == d["n_scp"] and not mir4
+            m["rk4_loop_mirrored"] = bool(mir4)
+            m["rk4_n_scp_oracle_loop"] = r4["n_scp"]
+            m["rk4_same_counts_so_far"] = same_counts4
+            m["rk4_loop_x0_diff"] = float(np.max(np.abs(r4["x0"] - d["x0"])))
+            m["rk4_loop_U_diff"] = float(np.max(np.abs(r4["U"] - d["U"])))
+            w4 = ref4.path[:, :, i * tps:(i + 1) * tps + 1].transpose(1, 2, 0)
+            m["rk4_loop_path_diff"] = float(np.max(np.abs(w4 - d["path"])))
         steps.append(m)
     return steps
 
 
-def run(case, B, steps, device, workers=16, mirror_steps=()):
+def run(case, B, steps, device, workers=16, mirror_steps=(), rk4_loop=False):
     x_init, recs = run_device(case, B, steps, device)
     ctx = mp.get_context("spawn")
-    tasks = [(case, x_init[b], recs[b], tuple(mirror_steps)) for b in range(B)]
+    tasks = [(case, x_init[b], recs[b], tuple(mirror_steps), rk4_loop) for b in range(B)]
     with ctx.Pool(min(workers, B)) as pool:
         per = pool.map(check_realisation, tasks)
     return per
@@ -184,4 +206,10 @@ def summary(per):
         loop_max_path_diff_same_counts=max((m["loop_path_diff"] for m in agree), default=0.0),
         loop_max_U_diff_same_counts=max((m["loop_U_diff"] for m in agree), default=0.0),
         loop_max_path_diff_all=max(m["loop_path_diff"] for m in allm),
-        loop_max_U_diff_all=max(m["loop_U_diff"] for m in allm))
+        loop_max_U_diff_all=max(m["loop_U_diff"] for m in allm),
+        **(dict(rk4_loop_steps_with_same_counts=sum(m["rk4_same_counts_so_far"] for m in allm),
+                rk4_loop_mirrored_steps=sum(m["rk4_loop_mirrored"] for m in allm),
+                rk4_loop_max_path_diff_all=max(m["rk4_loop_path_diff"] for m in allm),
+                rk4_loop_max_U_diff_all=max(m["rk4_loop_U_diff"] for m in allm),
+                rk4_loop_max_x0_diff_all=max(m["rk4_loop_x0_diff"] for m in allm))
+           if allm and "rk4_loop_path_diff" in allm[0] else {}))

@@ -31,6 +31,11 @@ CONFIGS = {
     "c5_circle4_mixed": (lambda: R.circle_scenario(4, Hp=30), 3, "faithful", (10, 20, 30), False),
     "frog_hp10": (lambda: R.frog_scenario(Hp=10), 2, "faithful", None, True),
     "parallel5_hp10": (lambda: R.parallel_scenario(5, Hp=10), 2, "faithful", None, True),
+    # per-iteration histories of the MFMA-factor configurations (round 3): c3 problem 0,
+    # and every problem of the c5 batch (one per horizon class 10 / 20 / 30, all in
+    # hp_max = 30 slots); the inputs are those of the fixtures above (same seed)
+    "c3_circle8_hp30_hist": (lambda: R.circle_scenario(8, Hp=30), 1, "structured", None, "all"),
+    "c5_circle4_mixed_hist": (lambda: R.circle_scenario(4, Hp=30), 3, "faithful", (10, 20, 30), "all"),
 }
 BASE_SEED = 20240
 
@@ -55,7 +60,8 @@ def make(name):
         nO = sc.nObst
         ob = bt.obst[b].reshape(-1)[:nO * 2 * H].reshape(nO, 2, H)
         p = R.make_problem(sc, bt.x0[b], bt.u0[b], bt.ec_noise[b], Hp=H, obst=ob)
-        r = R.scp_solve(p, mode=mode, keep_history=(hist and b == 0))
+        keep = hist == "all" or (hist and b == 0)
+        r = R.scp_solve(p, mode=mode, keep_history=keep)
         u[b, :nV * H] = r.u
         traj[b, :H * 2 * nV] = r.traj.reshape(-1)
         ref[b, :H * 2 * nV] = p.ref_points.reshape(-1)
@@ -65,17 +71,19 @@ def make(name):
             L = r.lin
             extra.update(lin_Ad=L.Ad, lin_Bd=L.Bd, lin_Ed=L.Ed, lin_g=L.g, lin_const=L.const,
                          lin_Phi0=L.Phi0, lin_Psi0=L.Psi0, lin_gamma0=L.gamma0)
-            if hist:
-                extra["hist_u_lin"] = np.array([h["u_lin"] for h in r.history])
-                extra["hist_A"] = np.array([h["A"] for h in r.history])
-                extra["hist_b"] = np.array([h["b"] for h in r.history])
-                extra["hist_z"] = np.array([h["z"] for h in r.history])
-                extra["hist_obj"] = np.array([h["obj"] for h in r.history])
-                extra["hist_maxviol"] = np.array([h["maxviol"] for h in r.history])
-                kkt = np.array([[h["certificate"][k] for k in
-                                 ("stationarity", "primal", "dual", "complementarity")]
-                                for h in r.history])
-                extra["hist_kkt"] = kkt
+        if keep:
+            # problem 0 under "hist_*", problem b > 0 under "hist{b}_*"
+            pre = "hist" if b == 0 else f"hist{b}"
+            extra[pre + "_u_lin"] = np.array([h["u_lin"] for h in r.history])
+            extra[pre + "_A"] = np.array([h["A"] for h in r.history])
+            extra[pre + "_b"] = np.array([h["b"] for h in r.history])
+            extra[pre + "_z"] = np.array([h["z"] for h in r.history])
+            extra[pre + "_obj"] = np.array([h["obj"] for h in r.history])
+            extra[pre + "_maxviol"] = np.array([h["maxviol"] for h in r.history])
+            kkt = np.array([[h["certificate"][k] for k in
+                             ("stationarity", "primal", "dual", "complementarity")]
+                            for h in r.history])
+            extra[pre + "_kkt"] = kkt
     out = os.path.join(HERE, name + ".npz")
     np.savez_compressed(out, scenario=name, mode=mode, n_veh=nV, n_obst=sc.nObst, hp_max=Hm,
                         x0=bt.x0, u0=bt.u0, ec_noise=bt.ec_noise, hp=bt.hp, obst=bt.obst,

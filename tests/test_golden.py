@@ -18,7 +18,13 @@ BUILDERS = {
     "c5_circle4_mixed": lambda: R.circle_scenario(4, Hp=30),
     "frog_hp10": lambda: R.frog_scenario(Hp=10),
     "parallel5_hp10": lambda: R.parallel_scenario(5, Hp=10),
+    "c3_circle8_hp30_hist": lambda: R.circle_scenario(8, Hp=30),
+    "c5_circle4_mixed_hist": lambda: R.circle_scenario(4, Hp=30),
 }
+# (fixture, problem) pairs with a per-iteration history; problem b > 0 under "hist{b}_*"
+HISTORIES = [("c1_circle1_hp10", 0), ("c2_circle4_hp20", 0), ("frog_hp10", 0),
+             ("parallel5_hp10", 0), ("c3_circle8_hp30_hist", 0), ("c5_circle4_mixed_hist", 0),
+             ("c5_circle4_mixed_hist", 1), ("c5_circle4_mixed_hist", 2)]
 
 
 def load(name):
@@ -54,26 +60,29 @@ def test_oracle_reproduces_fixture(name):
         assert np.max(np.abs(p.ref_points.reshape(-1) - f["ref_points"][b, :H * 2 * nV])) == 0.0
 
 
-@pytest.mark.parametrize("name", ["c1_circle1_hp10", "c2_circle4_hp20", "frog_hp10",
-                                  "parallel5_hp10"])
-def test_fixture_history_is_consistent(name):
+@pytest.mark.parametrize("name,pb", HISTORIES)
+def test_fixture_history_is_consistent(name, pb):
     f = load(name)
     sc = BUILDERS[name]()
-    p, H = problem(sc, f, 0)
+    p, H = problem(sc, f, pb)
     L = R.linearise(p, "structured")
     nV = sc.nVeh
     N = nV * H
-    assert len(f["hist_z"]) == f["n_scp"][0]
-    for it in range(len(f["hist_z"])):
-        A, b = R.linearised_rows_structured(p, L, f["hist_u_lin"][it])
-        assert np.max(np.abs(A - f["hist_A"][it]), initial=0.0) <= 1e-8
-        assert np.max(np.abs(b - f["hist_b"][it]), initial=0.0) <= 1e-8 * max(1, np.abs(b).max(initial=0))
-        kkt = f["hist_kkt"][it]
+    pre = "hist" if pb == 0 else f"hist{pb}"
+    hz = f[pre + "_z"]
+    assert len(hz) == f["n_scp"][pb]
+    for it in range(len(hz)):
+        A, b = R.linearised_rows_structured(p, L, f[pre + "_u_lin"][it])
+        assert np.max(np.abs(A - f[pre + "_A"][it]), initial=0.0) <= 1e-8
+        assert np.max(np.abs(b - f[pre + "_b"][it]), initial=0.0) <= 1e-8 * max(1, np.abs(b).max(initial=0))
+        kkt = f[pre + "_kkt"][it]
         assert kkt[1] <= 1e-9 and kkt[2] <= 1e-9
-        assert kkt[0] <= 1e-6 and kkt[3] <= 1e-7
-        z = f["hist_z"][it]
+        # stationarity and complementarity in unscaled units (multipliers up to the
+        # slack weight 1e5): 1e-6 absolute; c3 and c5 (Hp 30) reach 1.0e-6 and 1.5e-7
+        assert kkt[0] <= 1e-6 and kkt[3] <= (1e-7 if N <= 80 else 2e-6)
+        z = hz[it]
         assert np.all(np.abs(z[:N]) <= sc.uLim * (1 + 1e-9))
-    assert np.array_equal(f["hist_z"][-1][:N], f["u"][0, :N])
+    assert np.array_equal(hz[-1][:N], f["u"][pb, :N])
 
 
 def test_c3_fixture_structured():

@@ -6,6 +6,10 @@
   every problem, oracle parity (per SCP iteration on a stop flip) on 16 of them.
 * c3: 8 vehicles, Hp 30, B = 4096 (the LDS-pressure configuration); the same
   properties on all problems and oracle parity on 8 problems spread over the batch.
+* c5: 4 vehicles, mixed horizons Hp in {10, 20, 30} (problem g gets Hp[g mod 3]),
+  B = 3072 in hp_max = 30 slots (the divergent-wavefront stress configuration, per
+  problem early exit, SCP_controller.py:191-195); the properties on every problem
+  and per-iteration oracle parity on 6 problems of each horizon class.
 """
 import multiprocessing as mp
 
@@ -32,13 +36,13 @@ def _oracle_job(args):
         if p not in sys.path:
             sys.path.insert(0, p)
     from oracle import scp_reference as R_
-    n_veh, hp, x0, u0, ec = args
-    sc = R_.circle_scenario(n_veh, Hp=hp)
+    n_veh, hp, x0, u0, ec = args[:5]
+    sc = R_.circle_scenario(n_veh, Hp=args[5] if len(args) > 5 else hp)
     p = R_.make_problem(sc, x0, u0, ec, Hp=hp)
     return R_.scp_solve(p, mode="structured", keep_history=True)
 
 
-def _properties(S, sc, bt, out, nV, Hp):
+def _properties(S, sc, bt, out, nV, Hp, hp=None):
     u = out.u.cpu().numpy()
     st = out.status.cpu().numpy()
     ns = out.n_scp.cpu().numpy()
@@ -47,7 +51,7 @@ def _properties(S, sc, bt, out, nV, Hp):
     assert np.all((ns >= 1) & (ns <= 20))
     assert np.all(((st & 0xff) == LB.ST_CONVERGED) | ((st & 0xff) == LB.ST_MAX_SCP))
     # forward_U consistency on every problem: the evaluator on the returned u
-    ev = S.evaluate(out.u, bt.x0, bt.u0, bt.ec_noise)
+    ev = S.evaluate(out.u, bt.x0, bt.u0, bt.ec_noise, hp=hp)
     assert torch.max(torch.abs(ev["traj"] - out.traj)).item() <= 1e-12 * 30
     assert torch.allclose(ev["obj"], out.obj, rtol=1e-12, atol=0)
     assert torch.equal(ev["feasible"], out.feasible)
@@ -102,4 +106,32 @@ def test_c3_full_batch_4096(gpu):
     assert conv >= 0.8          # the reference's own 20-QP cap binds for ~12 % at c3
     idx = list(range(0, B, B // 8))
     _parity(out, bt, idx, 8, 30, workers=8)
+    S.close()
+
+
+def test_c5_mixed_horizon_full_batch_3072(gpu):
+    sc = R.circle_scenario(4, Hp=30)
+    B, Hs = 3072, (10, 20, 30)
+    bt = shard.shard_batch(sc, B, 0, base_seed=0, mixed_hp=Hs)
+    assert bt.hp_max == 30 and sorted(set(bt.hp.tolist())) == list(Hs)
+    S = ScpQpSolver(sc, max_batch=B, hp_max=30)
+    out = S.solve(bt.x0, bt.u0, bt.ec_noise, hp=bt.hp, trace=True)
+    torch.cuda.synchronize()
+    conv = _properties(S, sc, bt, out, 4, 30, hp=bt.hp)
+    assert conv >= 0.99
+    # outputs past a problem's own horizon stay untouched (zero-initialised slots)
+    u = out.u.cpu().numpy().reshape(B, -1)
+    for H in (10, 20):
+        sel = bt.hp == H
+        assert np.all(u[sel, 4 * H:] == 0.0)
+    # per-iteration parity: 6 problems of each horizon class, spread over the batch
+    idx = [b for H in Hs for b in np.flatnonzero(bt.hp == H)[::B // 3 // 6][:6].tolist()]
+    jobs = [(4, int(bt.hp[b]), bt.x0[b], bt.u0[b], bt.ec_noise[b], 30) for b in idx]
+    with mp.get_context("spawn").Pool(16) as pool:
+        res = pool.map(_oracle_job, jobs)
+    for b, r in zip(idx, res):
+        H = int(bt.hp[b])
+        ub, tb = unpack_problem(out, b, 4, H)
+        SP.compare(ub.cpu().numpy(), tb.cpu().numpy(), int(out.n_scp[b].item()),
+                   SP.device_trace(out, b, 4, 0, H, 30), r, 4, H, what=f"c5 problem {b} (Hp {H})")
     S.close()

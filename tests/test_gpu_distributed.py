@@ -102,3 +102,21 @@ def test_bench_two_ranks(gpu):
     assert d["n_gpus"] == 2 and d["steps"] == 2 and d["config"]["batch_per_gpu"] == 256
     # value = problems of BOTH ranks / max-over-ranks wall time
     assert d["value"] == pytest.approx(2 * 256 * 2 / (d["ms_per_step"] * 2 * 1e-3), rel=1e-9)
+
+
+def test_bench_spawns_ranks_itself(gpu):
+    """`python bench.py --gpus 2` with no launcher (the driver's plain form) starts both
+    ranks itself: one JSON line from rank 0 with n_gpus 2 aggregating both ranks.  On
+    this one-GPU box the ranks share the device, so the launcher picks gloo itself."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
+                        "SCPQP_DIST_BACKEND")}
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--no-cpu", "--batch", "256"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["batch_per_gpu"] == 256
+    assert d["value"] == pytest.approx(2 * 256 * 2 / (d["ms_per_step"] * 2 * 1e-3), rel=1e-9)

@@ -55,10 +55,17 @@ def cases():
         "c5_mixed": (R.circle_scenario(4, Hp=30), dict(mixed_hp=(10, 20, 30))),
         "frog": (R.frog_scenario(Hp=10), dict()),
         "parallel5": (R.parallel_scenario(5, Hp=10), dict()),
+        # mixed horizons WITH obstacles: the obstacle slot [nObst][2][hp_b] is read packed
+        # inside the hp_max slot (SCP_controller.py:106-114, MPC_Iter.py:45-51)
+        "frog_mixed": (R.frog_scenario(Hp=20), dict(mixed_hp=(10, 15, 20))),
+        "parallel5_mixed": (R.parallel_scenario(5, Hp=14), dict(mixed_hp=(6, 10, 14))),
     }
 
 
-@pytest.mark.parametrize("case", ["c2", "c5_mixed", "frog", "parallel5"])
+ALL_CASES = ["c2", "c5_mixed", "frog", "parallel5", "frog_mixed", "parallel5_mixed"]
+
+
+@pytest.mark.parametrize("case", ALL_CASES)
 def test_linearize_parity(gpu, case):
     sc, kw = cases()[case]
     bt = BT.make_batch(sc, 12, base_seed=101, **kw)
@@ -82,7 +89,7 @@ def test_linearize_parity(gpu, case):
     S.close()
 
 
-@pytest.mark.parametrize("case", ["c2", "c5_mixed", "frog", "parallel5"])
+@pytest.mark.parametrize("case", ALL_CASES)
 @pytest.mark.parametrize("quirk", [True, False])
 def test_evaluate_parity(gpu, case, quirk):
     sc, kw = cases()[case]
@@ -118,7 +125,7 @@ def test_evaluate_parity(gpu, case, quirk):
     S.close()
 
 
-@pytest.mark.parametrize("case", ["c2", "frog", "parallel5"])
+@pytest.mark.parametrize("case", ALL_CASES)
 def test_single_qp_parity(gpu, case):
     sc, kw = cases()[case]
     B = 32

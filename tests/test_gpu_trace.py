@@ -32,86 +32,108 @@ HIST = {
     "c2_circle4_hp20": lambda: R.circle_scenario(4, Hp=20),
     "frog_hp10": lambda: R.frog_scenario(Hp=10),
     "parallel5_hp10": lambda: R.parallel_scenario(5, Hp=10),
+    # the workspace-factor (MFMA trailing update) configurations: c3 (n = 241) and
+    # every horizon class of the mixed c5 batch (Hp 10 / 20 / 30 in hp_max = 30 slots)
+    "c3_circle8_hp30_hist": lambda: R.circle_scenario(8, Hp=30),
+    "c5_circle4_mixed_hist": lambda: R.circle_scenario(4, Hp=30),
 }
+# (fixture, problem): problem 0's history under "hist_*", problem b's under "hist{b}_*"
+CASES = [("c1_circle1_hp10", 0), ("c2_circle4_hp20", 0), ("frog_hp10", 0),
+         ("parallel5_hp10", 0), ("c3_circle8_hp30_hist", 0), ("c5_circle4_mixed_hist", 0),
+         ("c5_circle4_mixed_hist", 1), ("c5_circle4_mixed_hist", 2)]
 
 
 def _load(name):
     return dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
 
 
-@pytest.mark.parametrize("name", sorted(HIST))
-def test_trace_replays_golden_linearisations(gpu, name):
+def _hist(f, pb):
+    pre = "hist" if pb == 0 else f"hist{pb}"
+    return {k: f[pre + "_" + k] for k in ("u_lin", "A", "b", "z", "obj", "maxviol")}
+
+
+@pytest.mark.parametrize("name,pb", CASES)
+def test_trace_replays_golden_linearisations(gpu, name, pb):
     """One QP (max_scp_iter=1) from every recorded linearisation point of golden
-    problem 0: the device's rows equal hist_A/hist_b and its QP solution hist_z."""
+    problem pb: the device's rows equal hist_A/hist_b and its QP solution hist_z."""
     f = _load(name)
+    hs = _hist(f, pb)
     sc = HIST[name]()
-    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][0])
+    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][pb])
     N = nV * H
-    ul = f["hist_u_lin"]
+    Hm = int(f["hp_max"])
+    ul = hs["u_lin"]
     K = ul.shape[0]
-    rep = lambda a: np.repeat(a[0:1], K, axis=0)          # noqa: E731
-    S = ScpQpSolver(sc, max_batch=K, hp_max=int(f["hp_max"]))
+    rep = lambda a: np.repeat(a[pb:pb + 1], K, axis=0)          # noqa: E731
+    S = ScpQpSolver(sc, max_batch=K, hp_max=Hm)
     obst = rep(f["obst"]) if nO else None
-    out = S.solve(rep(f["x0"]), rep(f["u0"]), rep(f["ec_noise"]), obst=obst, u_warm=ul,
+    # u_warm slots hold [nVeh][hp_b] packed (include/scpqp.h): the vehicle-major
+    # iterate of length nVeh * H, zero-padded to the nVeh * hp_max slot
+    uw = np.zeros((K, nV * Hm))
+    uw[:, :N] = ul
+    hp = np.full(K, H, np.int32)
+    out = S.solve(rep(f["x0"]), rep(f["u0"]), rep(f["ec_noise"]), hp=hp, obst=obst, u_warm=uw,
                   max_scp_iter=1, trace=True)
-    lin = S.linearize(rep(f["x0"])[:1], rep(f["u0"])[:1], rep(f["ec_noise"])[:1])
+    lin = S.linearize(rep(f["x0"])[:1], rep(f["u0"])[:1], rep(f["ec_noise"])[:1], hp=hp[:1])
     torch.cuda.synchronize()
-    g = lin["g"][0].cpu().numpy()[:, :H]
+    g = lin["g"][0].cpu().numpy().reshape(-1)[:nV * H * 2].reshape(nV, H, 2)
     tr = out.trace.cpu().numpy()
     for it in range(K):
         d = TR.decode(tr[it], 1, nV, nO, H, S.hp_max, g=g, u_lim=S.u_lim)[0]
         assert np.array_equal(d["u_lin"], ul[it]), it          # the point the rows linearise at
-        A, b = f["hist_A"][it], f["hist_b"][it]
+        A, b = hs["A"][it], hs["b"][it]
         if A.shape[0]:
             sa = max(1.0, np.abs(A).max())
             assert np.max(np.abs(d["A"] - A)) <= 1e-9 * sa, it
             assert np.max(np.abs(d["b"] - b)) <= 1e-9 * max(1.0, np.abs(b).max()), it
-        z = f["hist_z"][it]
+        z = hs["z"][it]
         assert np.max(np.abs(d["z"][:N] - z[:N])) <= 1e-8, it   # one QP, same point (SURVEY §8d)
         assert abs(d["slack"] - z[N]) <= 1e-8 * max(1.0, abs(z[N])), it
         assert d["ipm_iters"] >= 0 and not d["warm"]
     S.close()
 
 
-@pytest.mark.parametrize("name", sorted(HIST))
-def test_trace_follows_golden_history(gpu, name):
-    """The device's own SCP iterates of golden problem 0 against hist_z / hist_obj /
+@pytest.mark.parametrize("name,pb", CASES)
+def test_trace_follows_golden_history(gpu, name, pb):
+    """The device's own SCP iterates of golden problem pb against hist_z / hist_obj /
     hist_maxviol, iteration by iteration, and the same stopping iteration."""
     f = _load(name)
+    hs = _hist(f, pb)
     sc = HIST[name]()
-    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][0])
+    nV, nO, H = sc.nVeh, sc.nObst, int(f["hp"][pb])
     N = nV * H
     S = ScpQpSolver(sc, max_batch=1, hp_max=int(f["hp_max"]))
-    obst = f["obst"][:1] if nO else None
-    out = S.solve(f["x0"][:1], f["u0"][:1], f["ec_noise"][:1], obst=obst, trace=True)
+    obst = f["obst"][pb:pb + 1] if nO else None
+    out = S.solve(f["x0"][pb:pb + 1], f["u0"][pb:pb + 1], f["ec_noise"][pb:pb + 1],
+                  hp=f["hp"][pb:pb + 1], obst=obst, trace=True)
     torch.cuda.synchronize()
     n = int(out.n_scp[0].item())
     tr = SP.device_trace(out, 0, nV, nO, H, S.hp_max)
-    K = f["hist_z"].shape[0]
+    K = hs["z"].shape[0]
     # the golden history's deltas: obj/maxviol of the iterates, starting from the
     # evaluation of the (eps-nudged) initial point (SCP_controller.py:77-79, 161)
-    p = R.make_problem(sc, f["x0"][0], f["u0"][0], f["ec_noise"][0], Hp=H,
-                       obst=f["obst"][0].reshape(-1)[:nO * 2 * H].reshape(nO, 2, H))
-    ev0 = R.evaluate_structured(p, R.linearise(p, "structured"), f["hist_u_lin"][0])
+    p = R.make_problem(sc, f["x0"][pb], f["u0"][pb], f["ec_noise"][pb], Hp=H,
+                       obst=f["obst"][pb].reshape(-1)[:nO * 2 * H].reshape(nO, 2, H))
+    ev0 = R.evaluate_structured(p, R.linearise(p, "structured"), hs["u_lin"][0])
     prev = ev0.obj + R.SLACK_WEIGHT * ev0.max_violation
     hist = []
     for it in range(K):
-        cur = float(f["hist_obj"][it]) + R.SLACK_WEIGHT * float(f["hist_maxviol"][it])
-        hist.append(dict(z=f["hist_z"][it], obj=float(f["hist_obj"][it]),
-                         maxviol=float(f["hist_maxviol"][it]), delta=prev - cur))
+        cur = float(hs["obj"][it]) + R.SLACK_WEIGHT * float(hs["maxviol"][it])
+        hist.append(dict(z=hs["z"][it], obj=float(hs["obj"][it]),
+                         maxviol=float(hs["maxviol"][it]), delta=prev - cur))
         prev = cur
     assert SP.stops(hist[-1]["delta"], hist[-1]["maxviol"], nV) or K == 20
     if n != K:
         class _R:        # the fixture in the shape of an oracle SCPResult
             n_scp, history = K, hist
-            u = f["u"][0, :N]
+            u = f["u"][pb, :N]
             traj = None
-        SP.compare(None, None, n, tr, _R, nV, H, what=name)
+        SP.compare(None, None, n, tr, _R, nV, H, what=f"{name}[{pb}]")
         K = min(n, K)
     for it in range(K):
-        assert np.max(np.abs(tr[it]["z"][:N] - f["hist_z"][it][:N])) <= SP.U_TOL, it
-        assert tr[it]["obj"] == pytest.approx(float(f["hist_obj"][it]), rel=1e-9, abs=1e-9)
-        assert tr[it]["maxviol"] == pytest.approx(float(f["hist_maxviol"][it]), rel=1e-7,
+        assert np.max(np.abs(tr[it]["z"][:N] - hs["z"][it][:N])) <= SP.U_TOL, it
+        assert tr[it]["obj"] == pytest.approx(float(hs["obj"][it]), rel=1e-9, abs=1e-9)
+        assert tr[it]["maxviol"] == pytest.approx(float(hs["maxviol"][it]), rel=1e-7,
                                                   abs=1e-10)
         if it + 1 < K:
             assert np.max(np.abs(tr[it + 1]["u_lin"] - tr[it]["z"][:N])) == 0.0

@@ -4,6 +4,7 @@ steps (tests/closed_loop_check.py does the work).
 
     python tools/closed_loop_parity.py main8 1 50      # main.py:234-255 configuration
     python tools/closed_loop_parity.py c2 16 50        # 16 perturbed c2 realisations
+    (main8, or --rk4: also the restated loop on the device's RK4 integrator)
 """
 import json
 import os
@@ -24,7 +25,9 @@ def main():
     out = sys.argv[4] if len(sys.argv) > 4 else f"gpurun_out/closed_loop_{case}.json"
     t = time.time()
     mirror = range(steps) if case == "main8" else ()
-    per = CC.run(case, B, steps, "cuda", workers=16, mirror_steps=mirror)
+    # main8: also the restated loop on the device's RK4 integrator (closed_loop_check 3.)
+    per = CC.run(case, B, steps, "cuda", workers=16, mirror_steps=mirror,
+                 rk4_loop=case == "main8" or "--rk4" in sys.argv)
     s = CC.summary(per)
     s.update(case=case, wall_s=time.time() - t)
     print(json.dumps(s, indent=1))

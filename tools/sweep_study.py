@@ -1,0 +1,292 @@
+"""CPU study: the convexified QP solved with an explicit inverse of the normal
+matrix (block sweep / Gauss-Jordan on the SPD matrix, pivot blocks of 4)
+instead of Cholesky + triangular solves.
+
+Question: does the IPM still converge in the same number of iterations, and
+does the polish (proximal multipliers on the active set) still certify the
+same minimiser, when every solve is a matvec with a swept inverse?  Run over
+the recorded SCP sequence of c2 problems (oracle history).
+
+    python tools/sweep_study.py [nprob] [block]        # explicit inverse (rejected)
+    python tools/sweep_study.py blocktri [nprob] [bs]   # block-inverse substitution (kept)
+
+Result (c2, 12 problems, 89 QPs): with the explicit inverse the IPM never reaches
+its 1e-9 tolerance (25.7 iterations on average against 14.8, every QP at the cap
+or broken down) and the polish certifies 47 of 89 QPs; one step of iterative
+refinement restores the iteration count but not the certification (58 of 89).
+The normal equations of the IPM are benignly ill-conditioned for Cholesky only.
+Block-inverse substitution (L D L' kept, the 8 x 8 diagonal blocks of L inverted
+explicitly): iteration counts, certification and answers equal to Cholesky's.
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd")]
+from oracle import scp_reference as R  # noqa: E402
+from scpqp import batch as BT  # noqa: E402
+
+
+def sweep_inverse(A, b=4):
+    """Block sweep of a symmetric positive definite matrix: returns inv(A)."""
+    A = A.copy()
+    n = A.shape[0]
+    for p0 in range(0, n, b):
+        P = slice(p0, min(n, p0 + b))
+        W = np.linalg.inv(A[P, P])
+        R_ = np.r_[0:p0, min(n, p0 + b):n]
+        ARP = A[np.ix_(R_, range(p0, min(n, p0 + b)))] @ W
+        A[np.ix_(R_, R_)] -= ARP @ A[np.ix_(range(p0, min(n, p0 + b)), R_)]
+        A[np.ix_(R_, range(p0, min(n, p0 + b)))] = ARP
+        A[np.ix_(range(p0, min(n, p0 + b)), R_)] = ARP.T
+        A[P, P] = -W
+    return -A
+
+
+class Inv:
+    def __init__(self, K, mode, blk):
+        self.mode = mode
+        if mode == "chol":
+            import scipy.linalg
+            self.L = scipy.linalg.cho_factor(K, lower=True)
+        else:
+            self.Ki = sweep_inverse(K, blk)
+            if not np.all(np.isfinite(self.Ki)) or np.any(np.diag(self.Ki) <= 0):
+                raise np.linalg.LinAlgError("sweep breakdown")
+            self.K = K
+
+    def solve(self, r):
+        if self.mode == "chol":
+            import scipy.linalg
+            return scipy.linalg.cho_solve(self.L, r)
+        x = self.Ki @ r
+        if self.mode == "inv+ir":   # one step of iterative refinement with K itself
+            x = x + self.Ki @ (r - self.K @ x)
+        return x
+
+
+def ipm(P, q, G, h, mode, blk, tol=1e-9, maxit=60):
+    mc = len(h)
+    x = Inv(P + G.T @ G, mode, blk).solve(-q + G.T @ h)
+    s = h - G @ x
+    lam = -s.copy()
+    ts = -s.min()
+    if ts >= -1e-8 * max(np.linalg.norm(s), 1.0):
+        s = s + (1 + ts)
+    tz = -lam.min()
+    if tz >= -1e-8 * max(np.linalg.norm(lam), 1.0):
+        lam = lam + (1 + tz)
+    qn = max(1.0, np.abs(q).max()); hn = max(1.0, np.abs(h).max())
+    for it in range(maxit):
+        rd = P @ x + q + G.T @ lam
+        rp = G @ x + s - h
+        gap = s @ lam
+        pobj = 0.5 * x @ P @ x + q @ x
+        if (np.abs(rp).max() <= tol * hn and np.abs(rd).max() <= tol * qn
+                and gap <= tol * max(1.0, abs(pobj))):
+            return x, s, lam, it, 1
+        mu = gap / mc
+        d = lam / s
+        try:
+            F = Inv(P + G.T @ (d[:, None] * G), mode, blk)
+        except np.linalg.LinAlgError:
+            return x, s, lam, it, 2
+
+        def solve(rc):
+            dx = F.solve(-rd - G.T @ (d * rp - rc / s))
+            ds = -rp - G @ dx
+            return dx, ds, -(rc + lam * ds) / s
+
+        dx, ds, dl = solve(s * lam)
+        a = R._max_step(s, ds, lam, dl)
+        sigma = ((s + a * ds) @ (lam + a * dl) / mc / mu) ** 3
+        dx, ds, dl = solve(s * lam + ds * dl - sigma * mu)
+        a = min(1.0, 0.99 * R._max_step(s, ds, lam, dl))
+        x = x + a * dx; s = s + a * ds; lam = lam + a * dl
+    return x, s, lam, maxit, 0
+
+
+def polish(P, q, G, h, x, s, lam, mode, blk, delta=3e-7, rho=1e-12, nref=40, rounds=6):
+    """qp_polish_regularised with the solves of `mode`; returns (x, lam, solves) or None."""
+    act = lam > s
+    y_all = np.where(act, lam, 0.0)
+    xk = x.copy()
+    F = None
+    extended = False
+    nsol = 0
+    for _ in range(rounds):
+        Ga, ha = G[act], h[act]
+        y = y_all[act].copy()
+        if F is None:
+            try:
+                F = Inv(P + rho * np.eye(len(q)) + Ga.T @ Ga / delta, mode, blk)
+            except np.linalg.LinAlgError:
+                return None
+        conv = False
+        for k in range(nref):
+            xn = F.solve(-q - Ga.T @ y + Ga.T @ ha / delta + rho * xk)
+            nsol += 1
+            y = y + (Ga @ xn - ha) / delta
+            step = np.abs(xn - xk).max()
+            xk = xn
+            if k >= 1 and step <= 1e-9 * max(1.0, np.abs(xk).max()):
+                conv = True
+                break
+        if not np.all(np.isfinite(xk)):
+            return None
+        ok, nxt = R._pdas_update(G, h, act, xk, y)
+        if ok and conv:
+            lam_full = np.zeros_like(lam); lam_full[act] = y
+            return xk, lam_full, nsol
+        y_all = np.zeros(len(h)); y_all[act] = y
+        if np.array_equal(nxt, act):
+            if conv or extended:
+                return None
+            extended = True
+            continue
+        y_all[~nxt] = 0.0
+        act = nxt
+        F = None
+    return None
+
+
+def main():
+    nprob = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    blk = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+    nveh = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    hp = int(sys.argv[4]) if len(sys.argv) > 4 else 20
+    sc = R.circle_scenario(nveh, Hp=hp)
+    bt = BT.make_batch(sc, nprob, base_seed=77)
+    N = nveh * hp
+    stats = {m: dict(it=[], fail=0, pol=0, nsol=[], err=[]) for m in ("chol", "inv", "inv+ir")}
+    for b in range(nprob):
+        p = R.make_problem(sc, bt.x0[b], bt.u0[b], bt.ec_noise[b], Hp=hp)
+        r = R.scp_solve(p, mode="structured", keep_history=True)
+        lin = R.linearise(p, "structured")
+        Phi0 = np.zeros((N, N)); Psi0 = np.zeros(N)
+        for v in range(nveh):
+            Phi0[hp * v:hp * (v + 1), hp * v:hp * (v + 1)] = lin.Phi0[v]
+            Psi0[hp * v:hp * (v + 1)] = lin.Psi0[v]
+        for hh in r.history:
+            P, q, G, h = R.qp_matrices(Phi0, Psi0, hh["A"], hh["b"], p.u_lim)
+            Ps, qs, Gs, hs, sv, rn = R.qp_scale(P, q, G, h, p.u_lim, N)
+            ref = R.qp_polish_exact(Ps, qs, Gs, hs, *R.qp_ipm(Ps, qs, Gs, hs)[:3])
+            for m, st in stats.items():
+                x, s, lam, it, code = ipm(Ps, qs, Gs, hs, m, blk)
+                st["it"].append(it)
+                st["fail"] += code != 1
+                pol = polish(Ps, qs, Gs, hs, x, s, lam, m, blk)
+                if pol is not None:
+                    st["pol"] += 1
+                    st["nsol"].append(pol[2])
+                    if ref is not None:
+                        st["err"].append(float(np.abs(pol[0] - ref[0]).max()))
+    nqp = len(stats["chol"]["it"])
+    print(f"{nprob} problems, {nqp} QPs (nveh {nveh}, Hp {hp}, block {blk})")
+    for m, st in stats.items():
+        e = np.array(st["err"]) if st["err"] else np.array([np.nan])
+        print(f"  {m:7s}: IPM its mean {np.mean(st['it']):.2f} max {max(st['it'])}, not converged "
+              f"{st['fail']}, polish certified {st['pol']}/{nqp}, solves/QP {np.mean(st['nsol']):.2f}, "
+              f"|x - exact| max {np.nanmax(e):.2e} p99 {np.nanpercentile(e, 99):.2e}")
+
+
+
+# ---------------------------------------------------------------------------------
+# Variant 2: keep L D L' but solve the triangular systems block-wise with explicit
+# inverses of the unit-lower diagonal blocks (block size bs): the dependency chain of
+# a solve becomes n / bs block steps instead of n row steps.
+def ldl(K):
+    n = K.shape[0]
+    L = np.eye(n); D = np.zeros(n); A = K.copy()
+    for j in range(n):
+        D[j] = A[j, j]
+        if not D[j] > 0:
+            raise np.linalg.LinAlgError("ldl breakdown")
+        L[j + 1:, j] = A[j + 1:, j] / D[j]
+        A[j + 1:, j + 1:] -= np.outer(L[j + 1:, j], L[j + 1:, j]) * D[j]
+    return L, D
+
+
+class BlockTri:
+    def __init__(self, K, bs):
+        self.L, self.D = ldl(K)
+        n = K.shape[0]
+        self.bs = bs
+        self.blocks = [(j, min(n, j + bs)) for j in range(0, n, bs)]
+        self.inv = [np.linalg.inv(self.L[a:b, a:b]) for a, b in self.blocks]   # unit lower
+
+    def solve(self, r):
+        L, D = self.L, self.D
+        y = r.copy()
+        for (a, b), Li in zip(self.blocks, self.inv):
+            y[a:b] = Li @ y[a:b]
+            y[b:] -= L[b:, a:b] @ y[a:b]
+        y /= D
+        x = y
+        for (a, b), Li in reversed(list(zip(self.blocks, self.inv))):
+            x[a:b] = Li.T @ x[a:b]
+            x[:a] -= L[a:b, :a].T @ x[a:b]
+        return x
+
+
+def study_blocktri(nprob=8, bs=8, nveh=4, hp=20):
+    global Inv
+    base_inv = Inv
+
+    class InvB(base_inv):
+        def __init__(self, K, mode, blk):
+            self.mode = mode
+            if mode == "chol":
+                return base_inv.__init__(self, K, mode, blk)
+            self.T = BlockTri(K, bs)
+
+        def solve(self, r):
+            if self.mode == "chol":
+                return base_inv.solve(self, r)
+            return self.T.solve(r)
+
+    Inv = InvB
+    sc = R.circle_scenario(nveh, Hp=hp)
+    bt = BT.make_batch(sc, nprob, base_seed=77)
+    N = nveh * hp
+    stats = {m: dict(it=[], fail=0, pol=0, nsol=[], err=[]) for m in ("chol", "blocktri")}
+    for b in range(nprob):
+        p = R.make_problem(sc, bt.x0[b], bt.u0[b], bt.ec_noise[b], Hp=hp)
+        r = R.scp_solve(p, mode="structured", keep_history=True)
+        lin = R.linearise(p, "structured")
+        Phi0 = np.zeros((N, N)); Psi0 = np.zeros(N)
+        for v in range(nveh):
+            Phi0[hp * v:hp * (v + 1), hp * v:hp * (v + 1)] = lin.Phi0[v]
+            Psi0[hp * v:hp * (v + 1)] = lin.Psi0[v]
+        for hh in r.history:
+            P, q, G, h = R.qp_matrices(Phi0, Psi0, hh["A"], hh["b"], p.u_lim)
+            Ps, qs, Gs, hs, sv, rn = R.qp_scale(P, q, G, h, p.u_lim, N)
+            ref = R.qp_polish_exact(Ps, qs, Gs, hs, *R.qp_ipm(Ps, qs, Gs, hs)[:3])
+            for m, st in stats.items():
+                x, s, lam, it, code = ipm(Ps, qs, Gs, hs, m, 4)
+                st["it"].append(it)
+                st["fail"] += code != 1
+                pol = polish(Ps, qs, Gs, hs, x, s, lam, m, 4)
+                if pol is not None:
+                    st["pol"] += 1
+                    st["nsol"].append(pol[2])
+                    if ref is not None:
+                        st["err"].append(float(np.abs(pol[0] - ref[0]).max()))
+    Inv = base_inv
+    nqp = len(stats["chol"]["it"])
+    print(f"block-triangular solves, block {bs}: {nprob} problems, {nqp} QPs")
+    for m, st in stats.items():
+        e = np.array(st["err"]) if st["err"] else np.array([np.nan])
+        print(f"  {m:8s}: IPM its mean {np.mean(st['it']):.2f} max {max(st['it'])}, not converged "
+              f"{st['fail']}, polish certified {st['pol']}/{nqp}, solves/QP {np.mean(st['nsol']):.2f}, "
+              f"|x - exact| max {np.nanmax(e):.2e}")
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "blocktri":
+        study_blocktri(int(sys.argv[2]) if len(sys.argv) > 2 else 8,
+                       int(sys.argv[3]) if len(sys.argv) > 3 else 8)
+    else:
+        main()
