@@ -242,9 +242,33 @@ struct Lay {
     VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
 };
 
-template <bool HG, bool VG, int RM, int OCC>
+// Problem shapes compiled as constants (template SH): the vehicle count, obstacle
+// count and horizon of the BASELINE configurations, so that every loop bound,
+// index division and LDS offset built from them folds at compile time (vehicle
+// loops unrolled, Toeplitz trip counts known).  0 = runtime shape (any problem);
+// a fixed horizon is used only when every problem of the launch has hp = hp_max.
+struct ShapeC {
+    int V, O, H;
+};
+__host__ __device__ constexpr ShapeC shape_c(int sh) {
+    return sh == 1 ? ShapeC{4, 0, 20}     // c2 / c4: 4 vehicles, Hp 20
+         : sh == 2 ? ShapeC{4, 0, 0}      // c5: 4 vehicles, mixed horizons
+         : sh == 3 ? ShapeC{8, 0, 30}     // c3: 8 vehicles, Hp 30
+                   : ShapeC{0, 0, 0};
+}
+template <int SH>
+__host__ __device__ __forceinline__ int shapeV(int v) { return shape_c(SH).V ? shape_c(SH).V : v; }
+template <int SH>
+__host__ __device__ __forceinline__ int shapeO(int o) { return shape_c(SH).V ? shape_c(SH).O : o; }
+template <int SH>
+__host__ __device__ __forceinline__ int shapeH(int h) { return shape_c(SH).H ? shape_c(SH).H : h; }
+
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
                                                     int O, int Hb) {
+    V = shapeV<SH>(V);
+    O = shapeO<SH>(O);
+    Hb = shapeH<SH>(Hb);
     Lay<HG, VG, RM, OCC> L;
     L.lead = 0;
     L.V = V; L.O = O; L.Hb = Hb; L.N = V * Hb; L.n = L.N + 1;
@@ -753,7 +777,7 @@ __device__ int setup_problem(const cKArgs& a, const cParams& P, const LT& L, int
 
 // Out-of-line setup: the trigonometry and expm constants stay out of the
 // register allocation of the solve loop.
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int b, int Hb) {
     // uniform arguments arrive in VGPRs: back to SGPRs (see uniform_ctx)
     ap = (const cKArgs*)readfirstlane_u64((unsigned long long)ap);
@@ -762,8 +786,8 @@ __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int 
     Hb = __builtin_amdgcn_readfirstlane(Hb);
     const cKArgs& a = *ap;
     const cParams& P = *(const cParams*)a.P;
-    const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
-    const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG);
+    const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
 }
 
@@ -1357,7 +1381,9 @@ __device__ bool cholesky(const LT& L) {
         const int sg = s % G;
         const int np = G == 1 ? 1 : (sg == 0 ? G : sg);
         const int jp = r0 - np * CB;   // < 0 at the first step: no look-ahead
-        const ldouble* dprev = dbuf + ((s - np) % (2 * G)) * CB;
+        // (s - np) & (2G - 1): a valid slot also at s < np (2G is a power of two), where
+        // jp < 0 and the pointer is not dereferenced
+        const ldouble* dprev = dbuf + ((s - np) & (2 * G - 1)) * CB;
         if (is_lead(L.lead)) {
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
@@ -1417,6 +1443,7 @@ __device__ bool cholesky(const LT& L) {
 #ifndef SCPQP_SCH
 #define SCPQP_SCH 4     // chunk of a factor in LDS
 #endif
+
 #ifndef SCPQP_SCH_G
 #define SCPQP_SCH_G 8   // chunk of a factor in the workspace: twice the steps cover the L2 latency
 #endif
@@ -1814,20 +1841,20 @@ __device__ __forceinline__ Ctx uniform_ctx(const Ctx& c) {
     return u;
 }
 
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
-    const Off f = plan_offsets(c.P->nV, c.P->nO, c.P->hpMax, HG, VG);
-    Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
+    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeH<SH>(c.P->hpMax), HG, VG);
+    Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
     L.lead = c.lead;
     return L;
 }
-#define PHASE template <bool HG, bool VG, int RM, int OCC> __device__ __noinline__
+#define PHASE template <bool HG, bool VG, int RM, int OCC, int SH> __device__ __noinline__
 #define LAYDEF                  \
     const Ctx cu_ = uniform_ctx(c); \
     const cParams& P = *cu_.P;  \
-    const Lay<HG, VG, RM, OCC> L = lay_of<HG, VG, RM, OCC>(cu_); \
+    const Lay<HG, VG, RM, OCC> L = lay_of<HG, VG, RM, OCC, SH>(cu_); \
     (void)P
-#define PH(f) f<HG, VG, RM, OCC>
+#define PH(f) f<HG, VG, RM, OCC, SH>
 
 PHASE void ph_assemble(Ctx c, double rho) {
     LAYDEF;
@@ -2209,7 +2236,7 @@ struct QpStats {
 // (primal-dual active set) and the round repeats.  Returns true if certified.
 // stall: give up once a correction changes no fewer rows than the one before
 // (warm rounds, see kWarmStall).
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, int max_rounds,
                                               int cap, double early, QpStats& st, bool stall = false) {
     bool ok = false, refactor = true, extended = false;
@@ -2261,7 +2288,7 @@ struct QpKnobs {
     int maxIpm, nRefine, mc;
     double ipmTol, polRho;
 };
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qflags, bool warm,
                                               QpStats& st) {
     const int mc = K.mc;
@@ -2270,7 +2297,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     if (warm) {
         PH(ph_polish_warm)(c);
         constexpr bool wide = HG && VG && RM == 4;
-        if (polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, wide ? SCPQP_WARM_ROUNDS_WIDE : kWarmRounds,
+        if (polish_rounds<HG, VG, RM, OCC, SH>(c, hmax, K.polRho, wide ? SCPQP_WARM_ROUNDS_WIDE : kWarmRounds,
                                            wide ? SCPQP_WARM_REFINE_WIDE : kWarmRefine,
                                            wide ? SCPQP_WARM_EARLY_WIDE : kWarmEarly, st,
                                            kWarmStall)) {
@@ -2317,12 +2344,12 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     if (!conv && it >= K.maxIpm) qflags |= SCPQP_FL_IPM_MAXIT;
     // ---- active-set polish on {lam > s}
     PH(ph_polish_prep)(c);
-    const bool ok = polish_rounds<HG, VG, RM, OCC>(c, hmax, K.polRho, kPolishRounds, K.nRefine,
+    const bool ok = polish_rounds<HG, VG, RM, OCC, SH>(c, hmax, K.polRho, kPolishRounds, K.nRefine,
                                                    INFINITY, st);
     if (!ok) qflags |= SCPQP_FL_POLISH_REJECTED;
     return ok;
 }
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, QpStats& st) {
     const Ctx c = uniform_ctx(c0);
     const cParams& P = *c.P;
@@ -2335,7 +2362,7 @@ __device__ __noinline__ bool qp_solve(Ctx c0, int* qflags, bool warm, QpStats& s
     K.polRho = P.polRho;
     QpStats ls{0, 0, 0, 0};
     int lf = 0;
-    const bool ok = qp_solve_body<HG, VG, RM, OCC>(c, K, lf, warm, ls);
+    const bool ok = qp_solve_body<HG, VG, RM, OCC, SH>(c, K, lf, warm, ls);
     st.ipm += ls.ipm;
     st.rounds += ls.rounds;
     st.refine += ls.refine;
@@ -2371,13 +2398,13 @@ __device__ __forceinline__ int lead_wave_elect(lint* sh) {
     return lead;
 }
 
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     ldouble* smem = (ldouble*)smem_;
     const cParams& P = *(const cParams*)a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
-    const Off f = plan_offsets(P.nV, P.nO, P.hpMax, HG, VG);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG);
     lint* slot = (lint*)(smem + f.red + 124);
     ldouble* lub = smem + f.ub;   // u-bar
     ldouble* lpb = smem + f.pb;   // positions of the last evaluated u
@@ -2413,7 +2440,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
         if (tid == 0 && b < 8192) g_ptime[2 * b] = __builtin_amdgcn_s_memrealtime();
 #endif
         PROF_T0();
-        const int sflag = setup_problem_ni<HG, VG, RM, OCC>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
+        const int sflag = setup_problem_ni<HG, VG, RM, OCC, SH>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
         PROF_ACC(10);
         const int sflag_any = __syncthreads_or(sflag);
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
@@ -2487,7 +2514,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             // active-set corrections to recover it (tools/polish_study.py: 0/16)
             const int ipm_before = qs.ipm;
             const bool warm_qp = warm_on && prev_ok && it >= 2;
-            prev_ok = qp_solve<HG, VG, RM, OCC>(c, &qflags, warm_qp, qs);
+            prev_ok = qp_solve<HG, VG, RM, OCC, SH>(c, &qflags, warm_qp, qs);
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
@@ -2584,6 +2611,8 @@ struct scpqp_handle {
 namespace {
 
 const size_t kLdsLimit = 163840;
+// workgroups per CU at three waves per SIMD (the 168-VGPR budget of OCC = 3)
+const int kMaxPerCU = 12 / NWAVE;
 
 int plan(scpqp_handle* h) {
     const int V = h->dims.n_veh, O = h->dims.n_obst, Hm = h->dims.hp_max;
@@ -2600,7 +2629,8 @@ int plan(scpqp_handle* h) {
         const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
         if (lds > kLdsLimit) continue;
         int perCU = (int)(kLdsLimit / lds);
-        if (perCU > 3) perCU = 3;   // beyond 3 the register budget, not LDS, bounds residency
+        // beyond 3 waves per SIMD the register budget, not LDS, bounds residency
+        if (perCU > kMaxPerCU) perCU = kMaxPerCU;
         if (perCU > bestPer) {
             best = cfg;
             bestPer = perCU;
@@ -2613,22 +2643,14 @@ int plan(scpqp_handle* h) {
     h->ldsBytes = (size_t)(f.persist + f.uni) * sizeof(double);
     h->wsStride = f.ws;
     h->grid = h->cus * bestPer;
-    h->occ = bestPer >= 3 ? 3 : 2;
-#ifdef SCPQP_OCC4
-    // diagnostic build: 4 workgroups per CU on plan 2 (matrix and vectors in the
-    // workspace), register budget compiled for 4 (128 VGPRs)
-    if (getenv("SCPQP_OCC4") && best == 2 && kLdsLimit / h->ldsBytes >= 4 &&
-        (V * Hm + 1 + 63) / 64 == 2) {
-        h->grid = h->cus * 4;
-        h->occ = 4;
-    }
-#endif
+    // waves per SIMD the register budget is compiled for (template OCC)
+    h->occ = (bestPer * NWAVE + 3) / 4 >= 3 ? 3 : 2;
     return 0;
 }
 
-template <bool HG, bool VG, int RM, int OCC>
+template <bool HG, bool VG, int RM, int OCC, int SH>
 int launch_t(scpqp_handle* h, const KArgs& a, hipStream_t st, int grid) {
-    auto kern = scp_kernel<HG, VG, RM, OCC>;
+    auto kern = scp_kernel<HG, VG, RM, OCC, SH>;
     HIPCHK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)h->ldsBytes));
     hipLaunchKernelGGL(kern, dim3(grid), dim3(NT), h->ldsBytes, st, a);
@@ -2659,25 +2681,43 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
-    const int occ = h->occ;   // workgroups per CU the register budget is compiled for
-#ifdef SCPQP_OCC4
-    if (occ == 4) return launch_t<true, true, 2, 4>(h, a, st, grid);
-#endif
+    const int occ = h->occ;   // waves per SIMD the register budget is compiled for
+    // compile-time shapes (shape_c): the BASELINE configurations' instantiations
+    const scpqp_dims& d = h->dims;
+    int sh = 0;
+    if (d.n_obst == 0 && d.n_veh == 4) sh = (d.hp_max == 20 && !a.hp) ? 1 : 2;
+    if (d.n_obst == 0 && d.n_veh == 8 && d.hp_max == 30 && !a.hp) sh = 3;
+    if (const char* e = getenv("SCPQP_SHAPE"))   // diagnostic: SCPQP_SHAPE=0 runs the runtime shape
+        if (atoi(e) == 0) sh = 0;
+#ifdef SCPQP_ONLY_C2
+    // diagnostic build (fast compile for A/B work): the c2 / c4 instantiations only
+    if (R != 2 || occ != 3 || h->hG || !h->vG)
+        return fail(SCPQP_E_SIZE, "SCPQP_ONLY_C2 build: c2-shaped problems only%s");
+    if (sh == 1) return launch_t<false, true, 2, 3, 1>(h, a, st, grid);
+    return launch_t<false, true, 2, 3, 0>(h, a, st, grid);
+#else
+    if (sh == 1 && !h->hG && h->vG && R == 2 && occ == 3) return launch_t<false, true, 2, 3, 1>(h, a, st, grid);
+    if (sh == 2 && h->vG && R == 2 && occ == 3) {
+        if (h->hG) return launch_t<true, true, 2, 3, 2>(h, a, st, grid);
+        return launch_t<false, true, 2, 3, 2>(h, a, st, grid);
+    }
+    if (sh == 3 && h->hG && R == 4 && occ == 2) return launch_t<true, true, 4, 2, 3>(h, a, st, grid);
 #define SCPQP_DISPATCH(HGV, VGV)                                              \
     switch (R * 4 + occ) {                                                   \
-        case 6: return launch_t<HGV, VGV, 1, 2>(h, a, st, grid);             \
-        case 7: return launch_t<HGV, VGV, 1, 3>(h, a, st, grid);             \
-        case 10: return launch_t<HGV, VGV, 2, 2>(h, a, st, grid);            \
-        case 11: return launch_t<HGV, VGV, 2, 3>(h, a, st, grid);            \
-        case 14: return launch_t<HGV, VGV, 3, 2>(h, a, st, grid);            \
-        case 15: return launch_t<HGV, VGV, 3, 3>(h, a, st, grid);            \
-        case 19: return launch_t<HGV, VGV, 4, 3>(h, a, st, grid);            \
-        default: return launch_t<HGV, VGV, 4, 2>(h, a, st, grid);            \
+        case 6: return launch_t<HGV, VGV, 1, 2, 0>(h, a, st, grid);          \
+        case 7: return launch_t<HGV, VGV, 1, 3, 0>(h, a, st, grid);          \
+        case 10: return launch_t<HGV, VGV, 2, 2, 0>(h, a, st, grid);         \
+        case 11: return launch_t<HGV, VGV, 2, 3, 0>(h, a, st, grid);         \
+        case 14: return launch_t<HGV, VGV, 3, 2, 0>(h, a, st, grid);         \
+        case 15: return launch_t<HGV, VGV, 3, 3, 0>(h, a, st, grid);         \
+        case 19: return launch_t<HGV, VGV, 4, 3, 0>(h, a, st, grid);         \
+        default: return launch_t<HGV, VGV, 4, 2, 0>(h, a, st, grid);         \
     }
     if (h->hG) { SCPQP_DISPATCH(true, true) }
     if (h->vG) { SCPQP_DISPATCH(false, true) }
     SCPQP_DISPATCH(false, false)
 #undef SCPQP_DISPATCH
+#endif
 }
 
 // need_obst: the entry point reads the obstacle predictions (solve, evaluate);

@@ -160,6 +160,12 @@ class ScpQpSolver:
         _need(u0, B * nV, "u0 [B, nVeh]")
         ec = self._dev(ec_noise)
         _need(ec, B * nV * 2, "ec_noise [B, nVeh, 2]")
+        if hp is not None and not isinstance(hp, torch.Tensor):
+            h = np.asarray(hp).reshape(-1)
+            if h.size == B and B and bool(np.all(h == Hm)):
+                # every problem at hp_max is the no-hp form: the kernel may then run the
+                # launch on its compiled-shape instantiation (csrc shape_c)
+                hp = None
         hpt = self._dev(hp, torch.int32)
         _need(hpt, B, "hp [B]")
         if need_obst and nO and obst is None:

@@ -132,7 +132,9 @@ def test_trace_follows_golden_history(gpu, name, pb):
         K = min(n, K)
     for it in range(K):
         assert np.max(np.abs(tr[it]["z"][:N] - hs["z"][it][:N])) <= SP.U_TOL, it
-        assert tr[it]["obj"] == pytest.approx(float(hs["obj"][it]), rel=1e-9, abs=1e-9)
+        # per-iteration objective at scp_parity's tolerance: the iterates agree to
+        # 1e-7 rad (U_TOL), which moves c3's ~6e3 objective by up to ~1e-9 relative
+        assert tr[it]["obj"] == pytest.approx(float(hs["obj"][it]), rel=SP.OBJ_RTOL, abs=1e-9)
         assert tr[it]["maxviol"] == pytest.approx(float(hs["maxviol"][it]), rel=1e-7,
                                                   abs=1e-10)
         if it + 1 < K:

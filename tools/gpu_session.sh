@@ -2,16 +2,19 @@
 # One GPU box session: A/B bench of library builds (bench.py, no CPU leg, two
 # alternating repetitions), then the GPU test suite on the shipped library.
 #   gpurun -- bash tools/gpu_session.sh <tag> "<cfg:steps ...>" "<lib.so ...>" [pytest -k expr | all | none]
-# Libraries built with -DSCPQP_ONLY_C2 serve c2-shaped problems only (c2, c4).
+# Libraries built with -DSCPQP_ONLY_C2 serve c2-shaped problems only (c2, c4).  A library
+# entry of the form VAR=value@lib.so runs that library with the environment variable set
+# (e.g. SCPQP_SHAPE=0@senquential-.../scpqp/libscpqp.so: the runtime-shape instantiation).
 TAG=$1; CFGS=$2; LIBS=$3; K=${4:-none}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 for rep in 1 2; do
   for cs in $CFGS; do
     c=${cs%%:*}; st=${cs##*:}
-    for lib in $LIBS; do
-      SCPQP_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu --config $c --steps $st --warmup 1 > $OUT/b.log 2>&1 || { tail -5 $OUT/b.log; exit 1; }
-      grep '^{' $OUT/b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c', '$lib', round(d['value']), round(d['roofline']['kernel_ms'],3), 'ipm/qp', round(d['mean_ipm_iters_per_qp'],2), 'conv', d['status_converged_frac'])" | tee -a $OUT/ab.txt
+    for ent in $LIBS; do
+      lib=${ent##*@}; envs=""; [ "$ent" != "$lib" ] && envs=${ent%%@*}
+      env $envs SCPQP_LIB=$PWD/$lib timeout -k 10 300 python bench.py --no-cpu --config $c --steps $st --warmup 1 > $OUT/b.log 2>&1 || { tail -5 $OUT/b.log; exit 1; }
+      grep '^{' $OUT/b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c', '$ent', round(d['value']), round(d['roofline']['kernel_ms'],3), 'ipm/qp', round(d['mean_ipm_iters_per_qp'],2), 'conv', d['status_converged_frac'])" | tee -a $OUT/ab.txt
     done
   done
 done
