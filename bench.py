@@ -43,9 +43,9 @@ import numpy as np  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD datasheet
 HBM_PEAK_GBS = 8000.0
 METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
-# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu_round2.sh + pmc_summary.py)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02_pmc_traffic_{}.json")
-PMC_SQ = os.path.join(ROOT, "profiles", "r02_pmc_sq_c2.json")
+# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu_measure.sh + pmc_summary.py)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03_pmc_traffic_{}.json")
+PMC_SQ = os.path.join(ROOT, "profiles", "r03_pmc_sq_{}.json")
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -268,18 +268,21 @@ def main():
 
     # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
     # workload at its default batch (tools/gpu_round2.sh + tools/pmc_summary.py)
-    traffic, sq = None, None
+    traffic, traffic_raw, sq = None, None, None
     default_b = {"c2": 1024, "c3": 4096, "c4": 8192, "c5": 3072}[args.config]
     tpath = PMC_TRAFFIC.format(args.config)
+    spath = PMC_SQ.format(args.config)
     if B == default_b and os.path.exists(tpath):
         try:
             with open(tpath) as fh:
-                traffic = json.load(fh).get("hbm_bytes_per_launch")
+                tj = json.load(fh)
+            traffic = tj.get("hbm_bytes_per_launch")
+            traffic_raw = tj.get("fetch_size_bytes_raw", 0.0) + tj.get("hbm_write_bytes_per_launch", 0.0)
         except (OSError, ValueError):
             traffic = None
-    if args.config == "c2" and B == default_b and os.path.exists(PMC_SQ):
+    if B == default_b and os.path.exists(spath):
         try:
-            with open(PMC_SQ) as fh:
+            with open(spath) as fh:
                 sq = json.load(fh)
         except (OSError, ValueError):
             sq = None
@@ -310,12 +313,19 @@ def main():
                      "kernel": "scp_kernel", "kernel_ms": kern_ms,
                      "traffic_source": f"profiles/{os.path.basename(tpath)} (FETCH_SIZE x2 + WRITE_SIZE)"
                      if traffic is not None else None,
+                     "traffic_raw_fetch": traffic_raw,
+                     "traffic_raw_note": "raw FETCH_SIZE + WRITE_SIZE (no x2 read correction; the true HBM "
+                                         "bytes lie between traffic_raw_fetch and traffic)"
+                     if traffic_raw is not None else None,
                      "hbm_achieved_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                      "hbm_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,
                      "lds_bank_conflict_ratio": sq["lds_bank_conflict_ratio"] if sq else None,
                      "sq_wait_any_frac": sq["wait_any_frac"] if sq else None,
-                     "sq_source": f"profiles/{os.path.basename(PMC_SQ)} (SQ_LDS_BANK_CONFLICT / "
-                                  f"SQ_LDS_IDX_ACTIVE, SQ_WAIT_ANY / SQ_WAVE_CYCLES)" if sq else None,
+                     "mfma_f64_insts_per_launch": sq.get("mfma_f64_insts") if sq else None,
+                     "mfma_flop_share": (sq.get("mfma_f64_flops", 0.0) / flops) if sq and flops else None,
+                     "sq_source": f"profiles/{os.path.basename(spath)} (SQ_LDS_BANK_CONFLICT / "
+                                  f"SQ_LDS_IDX_ACTIVE, SQ_WAIT_ANY / SQ_WAVE_CYCLES, "
+                                  f"SQ_INSTS_VALU_MFMA_F64 x 2048 FLOP)" if sq else None,
                      "memory_plan": res["plan"], "lds_bytes": res["lds_bytes"],
                      "workgroups": res["grid"],
                      "flops_per_launch": flops,
