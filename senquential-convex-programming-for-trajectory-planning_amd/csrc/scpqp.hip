@@ -133,6 +133,7 @@ struct KArgs {
     double* ws;
     long long wsStride;
     int* counter;
+    const int* perm;   // optional: work item w -> problem perm[w] (longest horizons first)
 };
 // The kernel argument block, addressed in the constant (kernarg) address space:
 // out-of-line functions take it by pointer without the copy to private memory
@@ -1108,6 +1109,14 @@ __device__ __forceinline__ int wave_id() {
     return __builtin_amdgcn_readfirstlane(threadIdx.x) >> 6;
 }
 __device__ __forceinline__ bool is_lead(int lead) { return wave_id() == lead; }
+// The lead's serial chains (panel factorisation, triangular solves) are the problem's
+// critical path; the other waves on its SIMD belong to other problems.  Raise the lead's
+// issue priority over them for the chain's duration (s_setprio; MI355X_MICROARCH.md,
+// "Two waves per SIMD": priority outranks age).
+// c2 84.7k -> 88.3k, c4 145k -> 149k solves/s (profiles/r03_ab_prio.txt).  Giving the
+// whole workgroup of a long-running problem priority instead (an age rule) changed nothing.
+__device__ __forceinline__ void lead_prio_up() { __builtin_amdgcn_s_setprio(2); }
+__device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0); }
 
 // Wave 0: factor the panel of columns [r0, r0 + jb) in registers, rows
 // i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB
@@ -1388,8 +1397,10 @@ __device__ bool cholesky(const LT& L) {
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
             ldouble* dn = dbuf + (s % (2 * G)) * CB;
+            lead_prio_up();
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
+            lead_prio_down();
         } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
@@ -1449,6 +1460,7 @@ __device__ bool cholesky(const LT& L) {
 #endif
 template <int R, class HP, int SCH>
 struct Solver {   // SCH: chunk (columns / rows) streamed per step group
+    static_assert(SCH % 2 == 0 && 64 % SCH == 0, "chunks tile the 64-row slots");
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
     int lane, n, ld;
@@ -1576,10 +1588,12 @@ __device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
     if (is_lead(L.lead)) {
         const int n = L.n;
         constexpr int RM = LT::RMAX;
+        lead_prio_up();
         if (RM == 1 || n <= 64) chol_solve_r<1>(L, bvec, x);
         else if (RM == 2 || n <= 128) chol_solve_r<(RM >= 2 ? 2 : 1)>(L, bvec, x);
         else if (RM == 3 || n <= 192) chol_solve_r<(RM >= 3 ? 3 : 1)>(L, bvec, x);
         else chol_solve_r<RM>(L, bvec, x);
+        lead_prio_down();
     }
     __syncthreads();
 }
@@ -2414,7 +2428,10 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     ldouble* lqs = smem + f.qs;
     const int lead = lead_wave_elect((lint*)(smem + f.red + 126));
     for (;;) {
-        if (tid == 0) slot[0] = atomicAdd(a.counter, 1);
+        if (tid == 0) {
+            const int w = atomicAdd(a.counter, 1);
+            slot[0] = (a.perm && w < a.B) ? a.perm[w] : w;
+        }
         __syncthreads();
         // problem index and horizon are workgroup-uniform: make them scalar so
         // every branch below that guards a barrier is a uniform (SALU) branch
@@ -2573,6 +2590,37 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Work order of a mixed-horizon batch (config c5): longest horizons first, so the
+// expensive problems start at once and the cheap ones fill the tail (LPT list
+// scheduling).  One workgroup: a counting sort of the problem indices by horizon,
+// descending; horizons outside [1, hp_max] go last.  The order within a horizon is
+// arbitrary (LDS atomics) and changes no result: every problem is solved on its own.
+// ---------------------------------------------------------------------------
+constexpr int kOrderThreads = 1024;
+__global__ __launch_bounds__(kOrderThreads) void order_kernel(const int* hp, int B, int hpMax, int* perm) {
+    __shared__ int cnt[SCPQP_MAX_HP + 2], off[SCPQP_MAX_HP + 2];
+    const int tid = threadIdx.x;
+    auto bucket = [&](int b) {
+        const int h = hp[b];
+        return (h >= 1 && h <= hpMax) ? h : 0;
+    };
+    for (int h = tid; h < SCPQP_MAX_HP + 2; h += kOrderThreads) cnt[h] = 0;
+    __syncthreads();
+    for (int b = tid; b < B; b += kOrderThreads) atomicAdd(&cnt[bucket(b)], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int start = 0;
+        for (int h = hpMax; h >= 1; --h) {
+            off[h] = start;
+            start += cnt[h];
+        }
+        off[0] = start;
+    }
+    __syncthreads();
+    for (int b = tid; b < B; b += kOrderThreads) perm[atomicAdd(&off[bucket(b)], 1)] = b;
+}
+
+// ---------------------------------------------------------------------------
 // Host side (left out of device-only probe builds: tools/probe/)
 // ---------------------------------------------------------------------------
 #ifdef SCPQP_NO_HOST
@@ -2600,6 +2648,7 @@ struct scpqp_handle {
     int device = 0;
     int cus = 256;
     int* counter = nullptr;
+    int* perm = nullptr;   // work order of mixed-horizon solves (order_kernel), max_batch ints
     double* ws = nullptr;
     size_t wsBytes = 0;
     int hG = 0, vG = 0, occ = 2;
@@ -2680,6 +2729,14 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.wsStride = h->wsStride;
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
+    a.perm = nullptr;
+    const char* ord = getenv("SCPQP_ORDER");   // diagnostic: SCPQP_ORDER=0 keeps the input order
+    if (a.mode == MODE_SOLVE && a.hp && h->perm && !(ord && atoi(ord) == 0)) {
+        hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, st, a.hp, a.B, h->dims.hp_max,
+                           h->perm);
+        HIPCHK(hipGetLastError());
+        a.perm = h->perm;
+    }
     const int R = (h->dims.n_veh * h->dims.hp_max + 1 + 63) / 64;   // row slots of the solves
     const int occ = h->occ;   // waves per SIMD the register budget is compiled for
     // compile-time shapes (shape_c): the BASELINE configurations' instantiations
@@ -2820,6 +2877,8 @@ int scpqp_create(const scpqp_dims* dims, const scpqp_params* p, int device, scpq
     if (e == hipSuccess) e = hipMalloc(&h->devP, sizeof(DevParams));
     if (e == hipSuccess) e = hipMemcpy(h->devP, &P, sizeof(DevParams), hipMemcpyHostToDevice);
     if (e == hipSuccess) e = hipMalloc(&h->counter, sizeof(int));
+    if (e == hipSuccess && dims->max_batch > 0)
+        e = hipMalloc(&h->perm, sizeof(int) * (size_t)dims->max_batch);
     if (e != hipSuccess) {
         snprintf(g_err, sizeof(g_err), "HIP error: %s", hipGetErrorString(e));
         scpqp_destroy(h);
@@ -2839,6 +2898,7 @@ int scpqp_destroy(scpqp_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->devP) (void)hipFree(h->devP);
     if (h->counter) (void)hipFree(h->counter);
+    if (h->perm) (void)hipFree(h->perm);
     if (h->ws) (void)hipFree(h->ws);
     delete h;
     return 0;
