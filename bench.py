@@ -267,7 +267,7 @@ def main():
     value = world * B * args.steps / elapsed
 
     # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # workload at its default batch (tools/gpu_round2.sh + tools/pmc_summary.py)
+    # workload at its default batch (tools/gpu_measure.sh + tools/pmc_summary.py)
     traffic, traffic_raw, sq = None, None, None
     default_b = {"c2": 1024, "c3": 4096, "c4": 8192, "c5": 3072}[args.config]
     tpath = PMC_TRAFFIC.format(args.config)

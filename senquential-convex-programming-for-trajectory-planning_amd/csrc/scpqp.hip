@@ -58,7 +58,7 @@ namespace {
 
 // Diagnostic phase stamps (built only with -DSCPQP_PROF; never in the shipped kernel).
 #ifdef SCPQP_PROF
-__device__ unsigned long long g_prof[24];
+__device__ unsigned long long g_prof[32];
 __device__ unsigned long long g_ptime[8192 * 2];   // per-problem [start, end] (100 MHz realtime)
 #define PROF_T0() unsigned long long _pt = __builtin_amdgcn_s_memtime()
 #define PROF_ACC(cat)                                                              \
@@ -85,13 +85,16 @@ __device__ unsigned long long g_ptime[8192 * 2];   // per-problem [start, end] (
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
 #define PROF_T0_FINE() PROF_T0()
 #define PROF_ACC_FINE(cat) PROF_ACC_LEAD(cat)
+#define PROF_ACC_FINE0(cat) PROF_ACC(cat)
 #else
 #define PROF_T0_FINE() (void)0
 #define PROF_ACC_FINE(cat) (void)0
+#define PROF_ACC_FINE0(cat) (void)0
 #endif
 
 typedef __attribute__((address_space(3))) double ldouble;
 typedef __attribute__((address_space(3))) int lint;
+typedef __attribute__((address_space(1))) int gint;
 typedef __attribute__((address_space(1))) double gdouble;
 typedef double double2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) double2v ldouble2;
@@ -171,7 +174,10 @@ struct Off {
     int ldAlloc, mcAlloc;
 };
 
-__host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool vG) {
+// lean (plan 1 at two workgroups per CU, OCC = 2): the W~ blocks and the constraint-row
+// arrays go to the workspace as well, so that a factor of up to ~7.6k entries (4
+// vehicles at Hp 30) stays in LDS with two workgroups per CU (= Lay::LEAN)
+__host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool vG, bool lean = false) {
     const int N = V * Hm, n = N + 1, m = V * (V - 1) / 2 * Hm + V * O * Hm;
     const int mc = m + 2 * N + 1, ld = n + ((6 - n % 4) % 4), nb = V * (V + 1) / 2;
     Off f;
@@ -188,10 +194,12 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.ya = p; p += pad2(2 * N);
     f.yb = p; p += pad2(2 * N);
     f.qs = p; p += pad2(N);
-    f.rowE = p; p += pad2(2 * m);
-    f.rowW = p; p += pad2(m);
-    f.rowH = p; p += pad2(m);
-    f.rinfo = p; p += pad2((m + 1) / 2);
+    int w = 0;
+    int& rp = lean ? w : p;   // constraint-row arrays: LDS, or the workspace (lean)
+    f.rowE = rp; rp += pad2(2 * m);
+    f.rowW = rp; rp += pad2(m);
+    f.rowH = rp; rp += pad2(m);
+    f.rinfo = rp; rp += pad2((m + 1) / 2);
     f.z = p; p += pad2(n);
     f.dz = p; p += pad2(n);
     f.rhs = p; p += pad2(n);
@@ -200,7 +208,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.red = p; p += 192;   // [0,64) reductions, 120 flag, 124 work slot, 126 lead, [128,192) pivots
     f.persist = p;
     f.scr = p;
-    int u = 0, w = 0;
+    int u = 0;
     // packed K plus one spare row (row n: target of the predicate-free tile stores)
     if (hG) { f.H = w; w += pad2(roff(n + 1) + 16); } else { f.H = p + u; u += pad2(roff(n + 1) + 16); }
     const int setup = NWAVE * SCR_PER_WAVE;
@@ -208,8 +216,8 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     // vehicles at Hp 30): the W~ blocks go to the workspace as well, and the setup
     // scratch (expm, dead before the first linearisation) shares the row arrays, so
     // the union is empty and two workgroups fit per CU
-    const bool wG = hG && vG && (n + 63) / 64 == 4;   // = Lay::WGLOBAL
-    const bool rows_scr = wG && f.rinfo + pad2((m + 1) / 2) - f.rowE >= setup;
+    const bool wG = (hG && vG && (n + 63) / 64 == 4) || lean;   // = Lay::WGLOBAL
+    const bool rows_scr = wG && !lean && f.rinfo + pad2((m + 1) / 2) - f.rowE >= setup;
     if (wG) { f.Wt = w; w += pad2(4 * Hm * nb); } else { f.Wt = p + u; u += pad2(4 * Hm * nb); }
     if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     f.uni = u > setup ? u : setup;
@@ -233,12 +241,17 @@ struct Lay {
     int V, O, Hb, N, n, m, mc, ld, mp, nb;
     int lead;   // the wave that runs the serial parts (panel, triangular solves)
     ldouble *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
-    ldouble *rowE, *rowW, *rowH, *z, *dz, *rhs, *rd, *dinv, *red, *scr;
+    ldouble *z, *dz, *rhs, *rd, *dinv, *red, *scr;
+    // lean plan 1 (two workgroups per CU): W~ and the constraint rows in the workspace
+    static constexpr bool LEAN = !HG && VG && OCC == 2;
     // W~ blocks: in the workspace on plan 2 for factors of 4 row slots (plan_offsets)
-    static constexpr bool WGLOBAL = HG && VG && RM == 4;
+    static constexpr bool WGLOBAL = (HG && VG && RM == 4) || LEAN;
     using WT = typename std::conditional<WGLOBAL, gdouble, ldouble>::type;
+    using RT = typename std::conditional<LEAN, gdouble, ldouble>::type;
+    using RIT = typename std::conditional<LEAN, gint, lint>::type;
+    RT *rowE, *rowW, *rowH;
+    RIT* rinfo;
     WT* Wt;
-    lint* rinfo;
     HT* H;
     VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
 };
@@ -280,12 +293,18 @@ __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* 
     L.nb = V * (V + 1) / 2;
     L.x0 = lds + f.x0; L.u0 = lds + f.u0; L.ec = lds + f.ec; L.g = lds + f.g; L.p0 = lds + f.p0;
     L.ref = lds + f.ref; L.ob = lds + f.ob; L.ub = lds + f.ub; L.pb = lds + f.pb;
-    L.ya = lds + f.ya; L.yb = lds + f.yb; L.qs = lds + f.qs; L.rowE = lds + f.rowE;
-    L.rowW = lds + f.rowW; L.rowH = lds + f.rowH; L.z = lds + f.z; L.dz = lds + f.dz;
+    L.ya = lds + f.ya; L.yb = lds + f.yb; L.qs = lds + f.qs;
+    if constexpr (Lay<HG, VG, RM, OCC>::LEAN) {
+        L.rowE = ws + f.rowE; L.rowW = ws + f.rowW; L.rowH = ws + f.rowH;
+        L.rinfo = (gint*)(ws + f.rinfo);
+    } else {
+        L.rowE = lds + f.rowE; L.rowW = lds + f.rowW; L.rowH = lds + f.rowH;
+        L.rinfo = (lint*)(lds + f.rinfo);
+    }
+    L.z = lds + f.z; L.dz = lds + f.dz;
     L.rhs = lds + f.rhs; L.rd = lds + f.rd; L.dinv = lds + f.dinv; L.red = lds + f.red;
     L.scr = lds + f.scr;
     if constexpr (Lay<HG, VG, RM, OCC>::WGLOBAL) L.Wt = ws + f.Wt; else L.Wt = lds + f.Wt;
-    L.rinfo = (lint*)(lds + f.rinfo);
     if constexpr (HG) L.H = ws + f.H; else L.H = lds + f.H;
     typename Lay<HG, VG, RM, OCC>::VT* vb;
     if constexpr (VG) vb = ws + f.vec; else vb = lds + f.vec;
@@ -787,7 +806,7 @@ __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int 
     Hb = __builtin_amdgcn_readfirstlane(Hb);
     const cKArgs& a = *ap;
     const cParams& P = *(const cParams*)a.P;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
     const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
 }
@@ -923,6 +942,9 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
 // own lower summation bound.  A tile's cost is its trip count Hb - TS max(lt, mt):
 // tiles are enumerated by decreasing cost and dealt to the threads in snake
 // order, so every thread gets about the same number of trips.
+#ifndef SCPQP_ASM_PREFETCH
+#define SCPQP_ASM_PREFETCH 1
+#endif
 template <int TS, class LT, class PD>
 __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD d, double rho) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb, N = L.N;
@@ -952,6 +974,26 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
         for (int i = 0; i < TS; ++i)
 #pragma unroll
             for (int j = 0; j < TS; ++j) c[i][j] = 0.0;
+#if SCPQP_ASM_PREFETCH
+        // software pipeline: the next step's g and W~ loads are in flight while this
+        // step's products run (the loop is LDS-latency-bound, not FMA-bound)
+        double2v an = ld2(ga + 2 * (k0 - l0)), bn = ld2(gb + 2 * (k0 - m0));
+        double2v wn0 = ld2(W + 4 * k0 * nb), wn1 = ld2(W + 4 * k0 * nb + 2);
+        for (int k = k0; k < Hb; ++k) {
+#pragma unroll
+            for (int i = TS - 1; i > 0; --i) {
+                av[i] = av[i - 1];
+                bv[i] = bv[i - 1];
+            }
+            av[0] = an;
+            bv[0] = bn;
+            const double2v w0 = wn0, w1 = wn1;
+            const int kn = k + 1 < Hb ? k + 1 : k;   // the last step reloads its own
+            an = ld2(ga + 2 * (kn - l0));
+            bn = ld2(gb + 2 * (kn - m0));
+            wn0 = ld2(W + 4 * kn * nb);
+            wn1 = ld2(W + 4 * kn * nb + 2);
+#else
         for (int k = k0; k < Hb; ++k) {
             if constexpr (TS == 2) {
                 // 2 x 2 (c2): reloading the second row / column measured ~1 % faster
@@ -970,6 +1012,7 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
                 bv[0] = ld2(gb + 2 * (k - m0));
             }
             const double2v w0 = ld2(W + 4 * k * nb), w1 = ld2(W + 4 * k * nb + 2);
+#endif
             double px[TS], py[TS];   // W~ g_b for every column
 #pragma unroll
             for (int j = 0; j < TS; ++j) {
@@ -1001,6 +1044,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     const double u2 = P.uLim * P.uLim;
     // phase 1: W~ blocks [k][a>=b] (2x2) and the omega-coupling vector in y-space (yb)
     const int nW = Hb * nb;
+    PROF_T0_FINE();
     for (int e = tid; e < nW + V * Hb; e += NT) {
         if (e < nW) {
             const int k = e / nb, ab = e % nb;
@@ -1049,6 +1093,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
     double red[4] = {ww, 0.0, 0.0, 0.0};
     block_reduce4<1>(red, 0, L.red);
+    PROF_ACC_FINE0(25);
     // phase 2: K_uu lower triangle in TS x TS tiles (assemble_tiles); 4 x 4 where
     // there are enough of them to give every thread two (only the workspace plans
     // have such horizons: the LDS-plan kernels do not carry the 4 x 4 registers)
@@ -1061,10 +1106,12 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
         (void)PV;
         assemble_tiles<2>(P, L, d, rho);
     }
+    PROF_ACC_FINE0(26);
     const int N = L.N;
     toeplitz_t_apply(L, L.yb, [&](int e, double tt) { L.H[roff(N) + e] = tt; });
     if (tid == 0) L.H[roff(N) + N] = red[0] + d[L.mc - 1] + rho;
     __syncthreads();
+    PROF_ACC_FINE0(27);
 }
 
 // ---------------------------------------------------------------------------
@@ -1086,6 +1133,9 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
 #define SCPQP_CB 8
 #endif
 #define CB SCPQP_CB
+#ifndef SCPQP_PANEL2
+#define SCPQP_PANEL2 1
+#endif
 static_assert(CB % 4 == 0 && CB <= 8, "panel width");
 
 // 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
@@ -1118,6 +1168,164 @@ __device__ __forceinline__ bool is_lead(int lead) { return wave_id() == lead; }
 __device__ __forceinline__ void lead_prio_up() { __builtin_amdgcn_s_setprio(2); }
 __device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0); }
 
+// Panel factorisation, round-3 form (SCPQP_PANEL2).  Same algorithm and operands as
+// panel_factor below, restructured to shorten the lead's dependency chain:
+//  * look-ahead from the most recent panel: its D-scaled rows r0 .. r0 + 7 were left in
+//    LDS (ldbuf, 8 x 8) by the previous step's lead, so they are read as broadcast
+//    loads instead of 64 v_readlane pairs; an older panel (grouped trailing update)
+//    still takes the readlane path;
+//  * the 8 x 8 diagonal block is gathered to every lane at once (36 independent
+//    readlanes) and factored on uniform values (L D L', right-looking), so the chain
+//    per column is the reciprocal and two FMAs instead of two readlane round trips;
+//  * every row then applies the block's factor by forward substitution
+//    (p_ic -= (p_ic' / D_c') U_cc', U = L D unscaled), which for the block's own rows
+//    repeats the uniform factorisation operation for operation.
+template <int RS, class HP>
+__device__ __forceinline__ void panel_factor2(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
+                                              const ldouble* dprev, ldouble* dout, lint* flag,
+                                              int nprev, ldouble* ldbuf) {
+    const int lane = threadIdx.x & 63;
+    PROF_T0_FINE();
+    double p[RS][CB];
+    int ro[RS];
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+        ro[t] = roff(i < n ? i : n - 1);
+#pragma unroll
+        for (int c = 0; c < CB; c += 2) {
+            const double2v v = ld2(H + ro[t] + r0 + c);
+            p[t][c] = v.x;
+            p[t][c + 1] = v.y;
+        }
+    }
+#ifdef SCPQP_PROF_FINE
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    PROF_ACC_FINE(18);
+    for (int q = 0; jp >= 0 && q < nprev; ++q) {
+        double li[RS][CB];
+#pragma unroll
+        for (int t = 0; t < RS; ++t)
+#pragma unroll
+            for (int c = 0; c < CB; c += 2) {
+                const double2v v = ld2(H + ro[t] + jp + q * CB + c);
+                li[t][c] = v.x;
+                li[t][c + 1] = v.y;
+            }
+        if (q == nprev - 1) {
+            // the previous step's D-scaled rows r0 + c, two columns per round
+#pragma unroll
+            for (int c = 0; c < CB; c += 2) {
+                double lk0[CB], lk1[CB];
+#pragma unroll
+                for (int c2 = 0; c2 < CB; c2 += 2) {
+                    const double2v v0 = ld2(ldbuf + c * CB + c2), v1 = ld2(ldbuf + (c + 1) * CB + c2);
+                    lk0[c2] = v0.x; lk0[c2 + 1] = v0.y;
+                    lk1[c2] = v1.x; lk1[c2 + 1] = v1.y;
+                }
+#pragma unroll
+                for (int t = 0; t < RS; ++t) {
+                    double s0 = li[t][0] * lk0[0], s1 = li[t][0] * lk1[0];
+#pragma unroll
+                    for (int c2 = 1; c2 < CB; ++c2) {
+                        s0 = fma(li[t][c2], lk0[c2], s0);
+                        s1 = fma(li[t][c2], lk1[c2], s1);
+                    }
+                    p[t][c] -= s0;
+                    p[t][c + 1] -= s1;
+                }
+            }
+        } else {
+            double ld[CB];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) ld[c] = li[0][c] * dprev[q * CB + c];
+#pragma unroll
+            for (int c = 0; c < CB; ++c) {
+                double lk[CB];
+#pragma unroll
+                for (int c2 = 0; c2 < CB; ++c2) lk[c2] = readlane_d(ld[c2], c);
+#pragma unroll
+                for (int t = 0; t < RS; ++t) {
+                    double sacc = 0.0;
+#pragma unroll
+                    for (int c2 = 0; c2 < CB; c2 += 2) sacc += li[t][c2] * lk[c2] + li[t][c2 + 1] * lk[c2 + 1];
+                    p[t][c] -= sacc;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+#pragma unroll
+        for (int c = 0; c < CB; ++c)
+            p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
+    }
+    PROF_ACC_FINE(19);
+    // the diagonal block (lanes 0 .. 7 of slot 0), lower triangle, on uniform values
+    double a[CB][CB];
+#pragma unroll
+    for (int c = 0; c < CB; ++c)
+#pragma unroll
+        for (int l = c; l < CB; ++l) a[l][c] = readlane_d(p[0][c], l);
+    double inv[CB];
+    int bad = 0;
+#pragma unroll
+    for (int c = 0; c < CB; ++c) {
+        const double D = a[c][c];
+        bad |= !(D > 0.0) || !isfinite(D);
+        inv[c] = recip(D);
+#pragma unroll
+        for (int l = c + 1; l < CB; ++l) {
+            const double lc = a[l][c] * inv[c];
+#pragma unroll
+            for (int m = c + 1; m <= l; ++m) a[l][m] -= lc * a[m][c];
+        }
+    }
+    // every row: forward substitution with the block's factor; u: unscaled entries
+    double u0[CB];   // slot 0's unscaled entries (the next step's look-ahead rows)
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+            if (t == 0) u0[c] = p[0][c];
+            const double lc = p[t][c] * inv[c];
+#pragma unroll
+            for (int c2 = c + 1; c2 < CB; ++c2) p[t][c2] -= lc * a[c2][c];
+            p[t][c] = lc;
+        }
+    }
+    if (lane < CB && lane < jb) {
+        double iv = inv[0], dv = a[0][0];
+#pragma unroll
+        for (int c = 1; c < CB; ++c) {
+            iv = lane == c ? inv[c] : iv;
+            dv = lane == c ? a[c][c] : dv;
+        }
+        dinv[r0 + lane] = iv;
+        dout[lane] = dv;
+    }
+    PROF_ACC_FINE(20);
+#pragma unroll
+    for (int t = 0; t < RS; ++t) {
+        const int i = r0 + lane + 64 * t;
+        if (i < n) {
+#pragma unroll
+            for (int c = 0; c < CB; c += 2)
+                if (c < jb && c <= lane + 64 * t) st2(H + ro[t] + r0 + c, double2v{p[t][c], p[t][c + 1]});
+        }
+    }
+    // rows r0 + 8 .. r0 + 15 (the next panel's diagonal-block rows), D-scaled, for the
+    // next step's look-ahead; the lead alone reads them, so no barrier is needed
+    if (lane >= CB && lane < 2 * CB) {
+#pragma unroll
+        for (int c = 0; c < CB; c += 2) st2(ldbuf + (lane - CB) * CB + c, double2v{u0[c], u0[c + 1]});
+    }
+    if (lane == 0) flag[0] = bad;
+    PROF_ACC_FINE(21);
+}
+
 // Wave 0: factor the panel of columns [r0, r0 + jb) in registers, rows
 // i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB
 // update of the previous panel (columns [jp, jp + CB), pivots dprev).
@@ -1127,7 +1335,12 @@ __device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0)
 template <int RS, class HP>
 __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
                                              const ldouble* dprev, ldouble* dout, lint* flag,
-                                             int nprev = 1) {
+                                             int nprev, ldouble* ldbuf) {
+#if SCPQP_PANEL2
+    panel_factor2<RS>(H, dinv, n, r0, jb, jp, dprev, dout, flag, nprev, ldbuf);
+    return;
+#endif
+    (void)ldbuf;
     const int lane = threadIdx.x & 63;
     PROF_T0_FINE();
     double p[RS][CB];
@@ -1381,6 +1594,7 @@ __device__ bool cholesky(const LT& L) {
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
     constexpr int G = (LT::HGLOBAL && SCPQP_MFMA_TRAIL) ? SCPQP_GROUP : 1;
     lint* flag = (lint*)(L.red + 120);   // [step parity]
+    ldouble* ldbuf = L.red;              // [CB][CB] look-ahead rows (panel_factor2; red is idle here)
     ldouble* dbuf = L.red + 128;         // pivots [step mod 2G][CB]; a group's slots are adjacent
     PROF_T0();
     for (int r0 = 0, s = 0; r0 < n; r0 += CB, ++s) {
@@ -1394,14 +1608,22 @@ __device__ bool cholesky(const LT& L) {
         // jp < 0 and the pointer is not dereferenced
         const ldouble* dprev = dbuf + ((s - np) & (2 * G - 1)) * CB;
         if (is_lead(L.lead)) {
+#ifdef SCPQP_PROBE_NOPANEL   // tools/probe/chol_probe.hip: time without the panel chain
+            if ((threadIdx.x & 63) == 0) flag[par] = 0;
+#else
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
             ldouble* dn = dbuf + (s % (2 * G)) * CB;
             lead_prio_up();
-            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
-            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np);
+            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
+            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             lead_prio_down();
-        } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n) {
+#endif
+        } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n
+#ifdef SCPQP_PROBE_NOTRAIL   // tools/probe/chol_probe.hip: time without the trailing update
+                   && r0 < 0
+#endif
+                   ) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
 #ifndef SCPQP_TRAIL_U2
@@ -1857,7 +2079,7 @@ __device__ __forceinline__ Ctx uniform_ctx(const Ctx& c) {
 
 template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
-    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeH<SH>(c.P->hpMax), HG, VG);
+    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeH<SH>(c.P->hpMax), HG, VG, !HG && VG && OCC == 2);
     Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
     L.lead = c.lead;
     return L;
@@ -2006,10 +2228,14 @@ __device__ __forceinline__ void update_body(const LT& L) {
 // it does not need the factor, so it is formed before the factorisation)
 PHASE void ph_scale_assemble_rhs(Ctx c) {
     LAYDEF;
+    PROF_T0_FINE();
     for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
     __syncthreads();
+    PROF_ACC_FINE0(24);
     assemble(P, L, L.dd, 0.0);
+    PROF_ACC_FINE0(29);
     newton_rhs_body(L, 0, 0.0);
+    PROF_ACC_FINE0(28);
 }
 // predictor back-substitution, affine step and centring, corrector right-hand side
 PHASE double ph_back_affine_rhs(Ctx c, double mu) {
@@ -2418,7 +2644,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     const cParams& P = *(const cParams*)a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
     lint* slot = (lint*)(smem + f.red + 124);
     ldouble* lub = smem + f.ub;   // u-bar
     ldouble* lpb = smem + f.pb;   // positions of the last evaluated u
@@ -2665,28 +2891,41 @@ const int kMaxPerCU = 12 / NWAVE;
 
 int plan(scpqp_handle* h) {
     const int V = h->dims.n_veh, O = h->dims.n_obst, Hm = h->dims.hp_max;
-    // Plans: 0 everything in LDS, 1 constraint vectors in the workspace, 2 also
-    // the KKT matrix.  Take the plan that fits the most workgroups per CU (the
-    // kernel is latency-bound: co-resident problems hide each other's waits);
-    // on a tie the one with less in global memory.  The register budget is
-    // compiled for 2 or 3 workgroups per CU (OCC).
+    // Plans: 0 everything in LDS, 1 constraint vectors in the workspace (lean at two
+    // workgroups per CU: W~ and the constraint rows too), 2 also the KKT matrix.  The
+    // register budget is compiled for 2 or 3 workgroups per CU (OCC), and the device
+    // runs plan 1 lean exactly when OCC = 2 (Lay::LEAN).  A plan with the factor in LDS
+    // is taken whenever it fits two workgroups per CU: its panel chain and trailing
+    // update run on LDS latencies, and with the factor in the workspace a problem is
+    // ~2.7x slower (4 vehicles at Hp 30: profiles/r03_c5_classes.txt); among the rest,
+    // the most workgroups per CU (the kernel is latency-bound), then less in global
+    // memory.
     const char* force = getenv("SCPQP_PLAN");   // diagnostic: force a plan
     const int cfg0 = force ? atoi(force) : 0, cfg1 = force ? cfg0 + 1 : 3;
-    int best = -1, bestPer = 0;
+    int best = -1, bestPer = 0, bestKey = -1;
+    bool bestLean = false;
     for (int cfg = cfg0; cfg < cfg1 && cfg < 3; ++cfg) {
-        const Off f = plan_offsets(V, O, Hm, cfg >= 2, cfg >= 1);
-        const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
-        if (lds > kLdsLimit) continue;
-        int perCU = (int)(kLdsLimit / lds);
-        // beyond 3 waves per SIMD the register budget, not LDS, bounds residency
-        if (perCU > kMaxPerCU) perCU = kMaxPerCU;
-        if (perCU > bestPer) {
-            best = cfg;
-            bestPer = perCU;
+        for (int ln = 0; ln < (cfg == 1 ? 2 : 1); ++ln) {
+            const bool lean = ln == 1;
+            const Off f = plan_offsets(V, O, Hm, cfg >= 2, cfg >= 1, lean);
+            const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
+            if (lds > kLdsLimit) continue;
+            int perCU = (int)(kLdsLimit / lds);
+            // beyond 3 waves per SIMD the register budget, not LDS, bounds residency
+            if (perCU > kMaxPerCU) perCU = kMaxPerCU;
+            if (cfg == 1 && !lean && perCU < 3) continue;   // OCC 2 runs plan 1 lean
+            if (lean && perCU > 2) perCU = 2;
+            const int key = ((cfg < 2 && perCU >= 2) ? 1000 : 0) + 10 * perCU + (2 - cfg);
+            if (key > bestKey) {
+                best = cfg;
+                bestPer = perCU;
+                bestKey = key;
+                bestLean = lean;
+            }
         }
     }
     if (best < 0) return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
-    const Off f = plan_offsets(V, O, Hm, best >= 2, best >= 1);
+    const Off f = plan_offsets(V, O, Hm, best >= 2, best >= 1, bestLean);
     h->hG = best >= 2;
     h->vG = best >= 1;
     h->ldsBytes = (size_t)(f.persist + f.uni) * sizeof(double);
@@ -2758,6 +2997,7 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
         if (h->hG) return launch_t<true, true, 2, 3, 2>(h, a, st, grid);
         return launch_t<false, true, 2, 3, 2>(h, a, st, grid);
     }
+    if (sh == 2 && !h->hG && h->vG && R == 2 && occ == 2) return launch_t<false, true, 2, 2, 2>(h, a, st, grid);
     if (sh == 3 && h->hG && R == 4 && occ == 2) return launch_t<true, true, 4, 2, 3>(h, a, st, grid);
 #define SCPQP_DISPATCH(HGV, VGV)                                              \
     switch (R * 4 + occ) {                                                   \
@@ -2982,9 +3222,9 @@ int scpqp_prof_times(unsigned long long* out, int n) {
     return 0;
 }
 int scpqp_prof_read(unsigned long long* out, int reset) {
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 24));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 32));
     if (reset) {
-        unsigned long long z[24] = {0};
+        unsigned long long z[32] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
     }
     return 0;

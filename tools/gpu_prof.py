@@ -6,7 +6,7 @@ PKG = os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning
 sys.path.insert(0, PKG)
 import numpy as np, torch
 from scpqp import _lib as LB
-lib = LB.load(os.path.join(PKG, "scpqp", "libscpqp_prof.so"))
+lib = LB.load(os.environ.get("SCPQP_PROF_LIB") or os.path.join(PKG, "scpqp", "libscpqp_prof.so"))
 LB._lib = lib
 lib.scpqp_prof_read.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 from oracle import scp_reference as R
@@ -16,7 +16,8 @@ names = ["ipm-loop-top", "residuals(first)", "scale+assemble+rhs", "cholesky", "
          "back+update+residuals", "polish-fact", "polish-refine", "chol_solve", "setup", "linearise",
          "chol:panel0", "chol:steps", "solve:fwd", "solve:bwd",   # 12-15: sub-phases of 3 / 9
          "ipm-init", "take_u+evaluate",
-         "panel:load", "panel:lookahead", "panel:pivots", "panel:store", "barrier-wait(w0)", "barrier-wait(w1)"]
+         "panel:load", "panel:lookahead", "panel:pivots", "panel:store", "barrier-wait(w0)", "barrier-wait(w1)",
+         "asm:d=lam/s", "asm:W~+reduce", "asm:tiles", "asm:toeplitz", "asm:newton-rhs", "asm:assemble", "(30)", "(31)"]
 CFGS = [(4, 20, 1), (4, 20, 1024), (8, 30, 1)]
 if len(sys.argv) > 1:   # e.g. 8:30:1024
     CFGS = [tuple(int(v) for v in a.split(":")) for a in sys.argv[1:]]
@@ -25,7 +26,7 @@ for nv, hp, B in CFGS:
     bt = BT.make_batch(sc, B, base_seed=1000)
     S = ScpQpSolver(sc, max_batch=B)
     S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
-    buf = (C.c_ulonglong * 24)()
+    buf = (C.c_ulonglong * 32)()
     lib.scpqp_prof_read(buf, 1)
     t = time.time()
     out = S.solve(bt.x0, bt.u0, bt.ec_noise); torch.cuda.synchronize()
