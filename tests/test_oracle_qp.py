@@ -97,3 +97,21 @@ def test_faithful_and_structured_scp_agree():
     assert a.n_scp == b.n_scp
     assert np.max(np.abs(a.u - b.u)) <= 1e-8
     assert np.max(np.abs(a.traj - b.traj)) <= 1e-7
+
+
+@pytest.mark.parametrize("n_veh,hp,seed", [(4, 12, 11), (3, 8, 1), (4, 10, 7)])
+def test_kernel_start_reaches_same_minimiser(n_veh, hp, seed):
+    """The HIP kernel's IPM starting point (ipm_start_omega): interior, and the IPM from it
+    polishes to the minimiser the CVXOPT start reaches (the QP's unique minimiser)."""
+    sc, (P, q, G, h), N = _qp_instance(n_veh, hp, seed)
+    Ps, qs, Gs, hs, sv, rn = R.qp_scale(P, q, G, h, sc.uLim, N)
+    x, s, lam = R.ipm_start_omega(Ps, qs, Gs, hs)
+    assert np.all(s > 0) and np.all(lam > 0)
+    assert x[N] >= 1.0 and lam[-1] == pytest.approx(R.SLACK_WEIGHT)
+    a = R.qp_ipm(Ps, qs, Gs, hs, init="cvxopt")
+    b = R.qp_ipm(Ps, qs, Gs, hs, init="omega")
+    assert b[4] in (1, 2)
+    pa = R.qp_polish_exact(Ps, qs, Gs, hs, *a[:3])
+    pb = R.qp_polish_exact(Ps, qs, Gs, hs, *b[:3])
+    assert pa is not None and pb is not None
+    assert np.max(np.abs(pa[0] - pb[0])) <= 1e-9
