@@ -2157,6 +2157,15 @@ PHASE void ph_init_a(Ctx c) {
 // CPU study, cold IPM iterations per QP (tools/ipm_corrector_study.py): c2 15.7 -> 12.5,
 // 4 veh Hp 10 14.3 -> 10.1, Hp 30 16.0 -> 13.0, parallel5 23.1 -> 18.0, frog 16.7 -> 14.7;
 // every QP's polish certifies the same minimiser.
+// A/B variant (SCPQP_INIT_ZERO): start the controls at 0 and skip the initial solve
+#ifndef SCPQP_INIT_ZERO
+#define SCPQP_INIT_ZERO 0
+#endif
+PHASE void ph_init_zero(Ctx c) {
+    LAYDEF;
+    for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] = 0.0;
+    __syncthreads();
+}
 PHASE void ph_init_decouple(Ctx c) {
     LAYDEF;
     const int N = L.N, o = roff(N);
@@ -2488,7 +2497,10 @@ PHASE void ph_trace_sol(Ctx c, double* dst, D4 ev, double delta, int ipm, int qf
 #define SCPQP_POLISH_EXTEND 1
 #endif
 constexpr int kPolishRounds = SCPQP_POLISH_ROUNDS;
-constexpr int kWarmRounds = 8;
+#ifndef SCPQP_WARM_ROUNDS
+#define SCPQP_WARM_ROUNDS 8
+#endif
+constexpr int kWarmRounds = SCPQP_WARM_ROUNDS;
 constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: P.nRefine)
 // Warm rounds stop refining as soon as the iterate shows the active set is
 // wrong (an inactive row violated, or an active multiplier negative, by more
@@ -2590,6 +2602,9 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     // ---- initial point: (P + G'G) x = -q + G'h (omega decoupled, see ph_init_b);
     // s = h - Gx and lam from ph_init_b
     PROF_T0();
+#if SCPQP_INIT_ZERO
+    PH(ph_init_zero)(c);
+#else
     PH(ph_init_a)(c);
     PH(ph_assemble)(c, 0.0);
 #if SCPQP_INIT_OMEGA
@@ -2598,6 +2613,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
     PH(ph_rhs_from_tv)(c, 0.0);
     PH(ph_solve)(c, 0);
+#endif
     PH(ph_init_b)(c);
     PROF_ACC(16);
     // ---- Mehrotra iterations
