@@ -773,8 +773,8 @@ def ipm_start_omega(P, q, G, h):
 def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60, init="cvxopt"):
     """Mehrotra predictor-corrector IPM for inequality QPs (CVXOPT coneqp class).
 
-    ``init``: 'cvxopt' (coneqp's default starting point) or 'omega' (the HIP
-    kernel's, ipm_start_omega).  Returns (x, s, lam, iterations, status) with
+    ``init``: 'cvxopt' (coneqp's default starting point and step rule) or 'omega'
+    (the HIP kernel's: ipm_start_omega and the step factor max(0.99, 1 - mu)).  Returns (x, s, lam, iterations, status) with
     status 1 = converged, 2 = normal-matrix Cholesky broke down (end of the
     central path reached numerically), 0 = iteration cap.
     """
@@ -816,7 +816,10 @@ def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60, init="cvxopt"):
         a = _max_step(s, ds, lam, dl)
         sigma = ((s + a * ds) @ (lam + a * dl) / mc / mu) ** 3
         dx, ds, dl = solve(s * lam + ds * dl - sigma * mu)
-        a = min(1.0, 0.99 * _max_step(s, ds, lam, dl))
+        # fraction to the boundary: 0.99 (coneqp); the kernel's round-3 rule max(0.99, 1 - mu)
+        # goes with its starting point (scpqp.hip step_factor)
+        eta = max(0.99, 1.0 - mu) if init == "omega" else 0.99
+        a = min(1.0, eta * _max_step(s, ds, lam, dl))
         x = x + a * dx; s = s + a * ds; lam = lam + a * dl
     return x, s, lam, maxit, 0
 

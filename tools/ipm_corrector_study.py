@@ -16,7 +16,9 @@ factor the iteration already has; an iteration costs the assembly, the
 factorisation, two solve pairs and two vector phases.  The cost model below
 uses the B = 1 phase stamps of the shipped kernel (profiles/r03_phases.txt).
 
-    python tools/ipm_corrector_study.py [n_problems]
+    python tools/ipm_corrector_study.py [n_problems] [c2|c3|hp10|hp30|frog|par5] [seed]
+
+The kernel's round-3 rules are "round-3 start + adaptive step" (DESIGN §3).
 """
 import os
 import sys
@@ -36,7 +38,8 @@ C_CORR = 10.5e3 + 14.5e3
 
 
 def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, maxit=60,
-        sig_pow=3, init="cvxopt", floor=1e-2, lam0=1.0, woff=1.0, shift=0.0, ulin=None, clip=0.9):
+        sig_pow=3, init="cvxopt", floor=1e-2, lam0=1.0, woff=1.0, shift=0.0, ulin=None, clip=0.9,
+        eta="fixed", lam_box=None):
     mc = len(h)
     x = np.linalg.solve(P + G.T @ G, -q + G.T @ h)
     s = h - G @ x
@@ -76,6 +79,8 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
         s = s + max(-1.5 * s.min(), 0.0) + (1.0 if init == "omega" else shift)
         s = np.maximum(s, floor * max(1.0, s.max()) if init == "omega-floor" else s)
         lam = np.full(len(h), lam0 if lam0 > 0 else -lam0 * abs(q[N]) / len(h))
+        if lam_box is not None:   # box rows: the rows without an omega coefficient
+            lam[:-1][col[:-1] == 0] = lam_box
         lam[-1] = abs(q[N]) / -col[-1]
         if init == "omega-bal":
             mu0 = (s @ lam) / len(h)
@@ -130,7 +135,12 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
                 dx, ds, dl, a = dx2, ds2, dl2, a2
             else:
                 break
-        a = min(1.0, 0.99 * a)
+        if eta == "fixed":
+            a = min(1.0, 0.99 * a)
+        elif eta == "adaptive":      # step factor max(0.99, 1 - mu)
+            a = min(1.0, max(0.99, 1.0 - mu) * a)
+        else:                        # max(0.95, 1 - 10 mu): damped further from the path
+            a = min(1.0, max(0.95, 1.0 - 10 * mu) * a)
         x = x + a * dx; s = s + a * ds; lam = lam + a * dl
     return x, s, lam, maxit, 0, ncorr
 
@@ -175,10 +185,18 @@ def main():
     new = dict(init="omega-floor", floor=0.1, lam0=-0.3)     # the kernel's starting point
     new = dict(init="omega-floor", floor=0.1, lam0=-0.3)     # the kernel's starting point
     new = dict(init="omega-floor", floor=0.1, lam0=-0.3)     # the kernel's starting point
-    variants = [("cvxopt init (round 2)", {}), ("omega init (kernel)", new),
-                ("lin init", dict(new, init="lin")), ("zero init", dict(new, init="zero")),
-                ("lin init floor .05", dict(new, init="lin", floor=0.05)),
-                ("lin init lam0 .2", dict(new, init="lin", lam0=-0.2))]
+    new = dict(init="omega-floor", floor=0.1, lam0=-0.3)     # the kernel's starting point
+    new = dict(init="omega-floor", floor=0.1, lam0=-0.3, eta="adaptive")   # the kernel (round 3)
+    new = dict(init="omega-floor", floor=0.1, lam0=-0.3, eta="adaptive")   # the kernel (round 3)
+    new = dict(init="omega-floor", floor=0.1, lam0=-0.3, eta="adaptive")   # the kernel (round 3)
+    start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
+    kernel = dict(start, eta="adaptive")                                   # + step_factor
+    variants = [("cvxopt start, 0.99 step (round 2)", {}), ("round-3 start, 0.99 step", start),
+                ("round-3 start + adaptive step", kernel),
+                ("  + 1 Gondzio corrector", dict(kernel, K=1)), ("  + sigma^2", dict(kernel, sig_pow=2)),
+                ("  slack floor .05", dict(kernel, floor=0.05)), ("  lam0 .2", dict(kernel, lam0=-0.2)),
+                ("  box-row lam0 10", dict(kernel, lam_box=10.0)),
+                ("  start at the linearisation point", dict(kernel, init="lin"))]
     base = None
     print(f"{len(qps)} QPs ({nprob} {scen} problems, every SCP iteration)")
     for name, kw in variants:
