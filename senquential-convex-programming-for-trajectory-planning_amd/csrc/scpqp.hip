@@ -979,6 +979,18 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
         // step's products run (the loop is LDS-latency-bound, not FMA-bound)
         double2v an = ld2(ga + 2 * (k0 - l0)), bn = ld2(gb + 2 * (k0 - m0));
         double2v wn0 = ld2(W + 4 * k0 * nb), wn1 = ld2(W + 4 * k0 * nb + 2);
+        // two steps ahead where g / W~ come from the workspace (plan 2: c3 5.36k -> 5.54k
+        // solves/s, profiles/r03_ab_prefetch.txt); one step for the LDS plans (c2, c5:
+        // within noise or slower)
+        constexpr bool PF2 = SCPQP_ASM_PREFETCH >= 2 || LT::HGLOBAL;
+        double2v an2 = an, bn2 = bn, wm0 = wn0, wm1 = wn1;
+        if constexpr (PF2) {
+            const int k1 = k0 + 1 < Hb ? k0 + 1 : k0;
+            an2 = ld2(ga + 2 * (k1 - l0));
+            bn2 = ld2(gb + 2 * (k1 - m0));
+            wm0 = ld2(W + 4 * k1 * nb);
+            wm1 = ld2(W + 4 * k1 * nb + 2);
+        }
         for (int k = k0; k < Hb; ++k) {
 #pragma unroll
             for (int i = TS - 1; i > 0; --i) {
@@ -988,11 +1000,23 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
             av[0] = an;
             bv[0] = bn;
             const double2v w0 = wn0, w1 = wn1;
-            const int kn = k + 1 < Hb ? k + 1 : k;   // the last step reloads its own
-            an = ld2(ga + 2 * (kn - l0));
-            bn = ld2(gb + 2 * (kn - m0));
-            wn0 = ld2(W + 4 * kn * nb);
-            wn1 = ld2(W + 4 * kn * nb + 2);
+            if constexpr (PF2) {
+                an = an2;
+                bn = bn2;
+                wn0 = wm0;
+                wn1 = wm1;
+                const int kn = k + 2 < Hb ? k + 2 : Hb - 1;
+                an2 = ld2(ga + 2 * (kn - l0));
+                bn2 = ld2(gb + 2 * (kn - m0));
+                wm0 = ld2(W + 4 * kn * nb);
+                wm1 = ld2(W + 4 * kn * nb + 2);
+            } else {
+                const int kn = k + 1 < Hb ? k + 1 : k;   // the last step reloads its own
+                an = ld2(ga + 2 * (kn - l0));
+                bn = ld2(gb + 2 * (kn - m0));
+                wn0 = ld2(W + 4 * kn * nb);
+                wn1 = ld2(W + 4 * kn * nb + 2);
+            }
 #else
         for (int k = k0; k < Hb; ++k) {
             if constexpr (TS == 2) {

@@ -139,6 +139,8 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
             a = min(1.0, 0.99 * a)
         elif eta == "adaptive":      # step factor max(0.99, 1 - mu)
             a = min(1.0, max(0.99, 1.0 - mu) * a)
+        elif isinstance(eta, tuple):  # (floor, scale): max(floor, 1 - scale * mu)
+            a = min(1.0, max(eta[0], 1.0 - eta[1] * mu) * a)
         else:                        # max(0.95, 1 - 10 mu): damped further from the path
             a = min(1.0, max(0.95, 1.0 - 10 * mu) * a)
         x = x + a * dx; s = s + a * ds; lam = lam + a * dl
@@ -191,12 +193,19 @@ def main():
     new = dict(init="omega-floor", floor=0.1, lam0=-0.3, eta="adaptive")   # the kernel (round 3)
     start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
     kernel = dict(start, eta="adaptive")                                   # + step_factor
+    start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
+    kernel = dict(start, eta="adaptive")                                   # + step_factor
+    start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
+    kernel = dict(start, eta="adaptive")                                   # + step_factor
     variants = [("cvxopt start, 0.99 step (round 2)", {}), ("round-3 start, 0.99 step", start),
                 ("round-3 start + adaptive step", kernel),
                 ("  + 1 Gondzio corrector", dict(kernel, K=1)), ("  + sigma^2", dict(kernel, sig_pow=2)),
                 ("  slack floor .05", dict(kernel, floor=0.05)), ("  lam0 .2", dict(kernel, lam0=-0.2)),
                 ("  box-row lam0 10", dict(kernel, lam_box=10.0)),
-                ("  start at the linearisation point", dict(kernel, init="lin"))]
+                ("  start at the linearisation point", dict(kernel, init="lin")),
+                ("  step max(.99, 1 - .1 mu)", dict(start, eta=(0.99, 0.1))),
+                ("  step max(.995, 1 - mu)", dict(start, eta=(0.995, 1.0))),
+                ("  step max(.95, 1 - 10 mu)", dict(start, eta="damped"))]
     base = None
     print(f"{len(qps)} QPs ({nprob} {scen} problems, every SCP iteration)")
     for name, kw in variants:
