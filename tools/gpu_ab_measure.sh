@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round-3 closing session, one box: an A/B of a candidate build (one repetition), then the
+# Closing session of a round, one box: an A/B of a candidate build (one repetition), then the
 # measurement records of the shipped library (tools/gpu_measure.sh: rocprofv3 kernel stats,
 # SQ / MFMA / FETCH / WRITE passes per config, phase stamps and the c2 timeline).
-#   gpurun --timeout 1200 -- bash tools/gpu_final_r03.sh <tag> "<candidate.so ...>"
+#   gpurun --timeout 1200 -- bash tools/gpu_ab_measure.sh <tag> "<candidate.so ...>"
 set -u
 TAG=$1; CAND=${2:-}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
