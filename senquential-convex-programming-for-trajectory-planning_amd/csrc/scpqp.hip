@@ -2336,6 +2336,24 @@ PHASE void ph_scale_assemble_rhs(Ctx c) {
     newton_rhs_body(L, 0, 0.0);
     PROF_ACC_FINE0(28);
 }
+// the same, then L D L' of K in the same call (SCPQP_FUSE_FACT); 1 = factored
+#ifndef SCPQP_FUSE_FACT
+#define SCPQP_FUSE_FACT 0
+#endif
+PHASE int ph_scale_assemble_rhs_factor(Ctx c) {
+    LAYDEF;
+    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
+    __syncthreads();
+    assemble(P, L, L.dd, 0.0);
+    newton_rhs_body(L, 0, 0.0);
+    return cholesky(L) ? 1 : 0;
+}
+// polish: K = P + rho I + G_A' G_A / delta, factored in the same call
+PHASE int ph_assemble_factor(Ctx c, double rho) {
+    LAYDEF;
+    assemble(P, L, L.dd, rho);
+    return cholesky(L) ? 1 : 0;
+}
 // predictor back-substitution, affine step and centring, corrector right-hand side
 PHASE double ph_back_affine_rhs(Ctx c, double mu) {
     LAYDEF;
@@ -2348,6 +2366,31 @@ PHASE double ph_back_affine_rhs(Ctx c, double mu) {
 // point (the next iteration's convergence test)
 PHASE D4 ph_back_update_residuals(Ctx c, double smu, double eta) {
     LAYDEF;
+    newton_back_body(L, 1, smu);
+    update_body(L, eta);
+    double r[4];
+    residuals(P, L, r);
+    return D4{r[0], r[1], r[2], r[3]};
+}
+// Fused solve phases (round 3, SCPQP_FUSE_SOLVE): the triangular solve and the vector
+// phase after it in one out-of-line call.  A call costs its callee-saved register
+// spills and restores through the private stack (280 B per lane, the source of c2's
+// write traffic) and the layout rebuild; the two bodies run one after the other, so
+// the fused function's register budget is the larger of the two, not their sum.
+#ifndef SCPQP_FUSE_SOLVE
+#define SCPQP_FUSE_SOLVE 0
+#endif
+PHASE double ph_solve_back_affine_rhs(Ctx c, double mu) {
+    LAYDEF;
+    chol_solve(L, L.rhs, L.dz);
+    newton_back_body(L, 0, 0.0);
+    const double smu = affine_body(L, mu);
+    newton_rhs_body(L, 1, smu);
+    return smu;
+}
+PHASE D4 ph_solve_back_update_residuals(Ctx c, double smu, double eta) {
+    LAYDEF;
+    chol_solve(L, L.rhs, L.dz);
     newton_back_body(L, 1, smu);
     update_body(L, eta);
     double r[4];
@@ -2434,6 +2477,13 @@ __device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
 // ends the refinement here, the next right-hand side in the same call
 PHASE D4 ph_polish_dual_next(Ctx c, int ref, int cap, double early) {
     LAYDEF;
+    const D4 d = polish_dual_body(P, L);
+    if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
+    return d;
+}
+PHASE D4 ph_solve_polish_dual_next(Ctx c, int ref, int cap, double early) {
+    LAYDEF;
+    chol_solve(L, L.rhs, L.dz);
     const D4 d = polish_dual_body(P, L);
     if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
     return d;
@@ -2576,16 +2626,24 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, in
     for (int round = 0; round < max_rounds && !ok; ++round) {
         ++st.rounds;
         if (refactor) {
+#if SCPQP_FUSE_FACT
+            const bool fact = PH(ph_assemble_factor)(c, rho) != 0;
+#else
             PH(ph_assemble)(c, rho);
             const bool fact = PH(ph_cholesky)(c) != 0;
+#endif
             PROF_ACC(7);
             if (!fact) break;
         }
         int conv = 0;
         PH(ph_polish_rhs)(c);
         for (int ref = 0; ref < cap; ++ref) {
+#if SCPQP_FUSE_SOLVE
+            const D4 d = PH(ph_solve_polish_dual_next)(c, ref, cap, early);
+#else
             PH(ph_solve)(c, 1);
             const D4 d = PH(ph_polish_dual_next)(c, ref, cap, early);
+#endif
             ++st.refine;
             const int stop = polish_stop(d, ref, early);
             conv = stop == 1;
@@ -2664,10 +2722,21 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
                 break;
             }
             const double mu = res.c / mc;
+#if SCPQP_FUSE_FACT
+            if (!PH(ph_scale_assemble_rhs_factor)(c)) break;
+            PROF_ACC(3);
+#else
             PH(ph_scale_assemble_rhs)(c);
             PROF_ACC(2);
             if (!PH(ph_cholesky)(c)) break;
             PROF_ACC(3);
+#endif
+#if SCPQP_FUSE_SOLVE
+            const double smu = PH(ph_solve_back_affine_rhs)(c, mu);
+            PROF_ACC(5);
+            res = PH(ph_solve_back_update_residuals)(c, smu, step_factor(mu));
+            PROF_ACC(6);
+#else
             PH(ph_solve)(c, 1);
             PROF_ACC(9);
             const double smu = PH(ph_back_affine_rhs)(c, mu);
@@ -2676,6 +2745,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
             PROF_ACC(9);
             res = PH(ph_back_update_residuals)(c, smu, step_factor(mu));
             PROF_ACC(6);
+#endif
         }
         // ---- active-set polish on {lam > s}
         PH(ph_polish_prep)(c);

@@ -39,7 +39,7 @@ C_CORR = 10.5e3 + 14.5e3
 
 def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, maxit=60,
         sig_pow=3, init="cvxopt", floor=1e-2, lam0=1.0, woff=1.0, shift=0.0, ulin=None, clip=0.9,
-        eta="fixed", lam_box=None):
+        eta="fixed", lam_box=None, start=None):
     mc = len(h)
     x = np.linalg.solve(P + G.T @ G, -q + G.T @ h)
     s = h - G @ x
@@ -92,6 +92,8 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
         lam = lam + max(-1.5 * lam.min(), 0.0) + 1e-8
         sl = s @ lam
         s, lam = s + 0.5 * sl / lam.sum(), lam + 0.5 * sl / s.sum()
+    if start is not None:            # explicit (x, s, lam), e.g. a warm start
+        x, s, lam = (np.array(v, float) for v in start)
     qn = max(1.0, np.abs(q).max()); hn = max(1.0, np.abs(h).max())
     ncorr = 0
     for it in range(maxit):
