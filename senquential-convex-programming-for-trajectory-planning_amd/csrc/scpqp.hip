@@ -2338,7 +2338,7 @@ PHASE void ph_scale_assemble_rhs(Ctx c) {
 }
 // the same, then L D L' of K in the same call (SCPQP_FUSE_FACT); 1 = factored
 #ifndef SCPQP_FUSE_FACT
-#define SCPQP_FUSE_FACT 0
+#define SCPQP_FUSE_FACT 1
 #endif
 PHASE int ph_scale_assemble_rhs_factor(Ctx c) {
     LAYDEF;
