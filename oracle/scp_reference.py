@@ -774,7 +774,8 @@ def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60, init="cvxopt"):
     """Mehrotra predictor-corrector IPM for inequality QPs (CVXOPT coneqp class).
 
     ``init``: 'cvxopt' (coneqp's default starting point and step rule) or 'omega'
-    (the HIP kernel's: ipm_start_omega and the step factor max(0.99, 1 - mu)).  Returns (x, s, lam, iterations, status) with
+    (the HIP kernel's: ipm_start_omega, the step factor max(0.99, 1 - mu) and separate
+    primal and dual step lengths).  Returns (x, s, lam, iterations, status) with
     status 1 = converged, 2 = normal-matrix Cholesky broke down (end of the
     central path reached numerically), 0 = iteration cap.
     """
@@ -819,6 +820,11 @@ def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60, init="cvxopt"):
         # fraction to the boundary: 0.99 (coneqp); the kernel's round-3 rule max(0.99, 1 - mu)
         # goes with its starting point (scpqp.hip step_factor)
         eta = max(0.99, 1.0 - mu) if init == "omega" else 0.99
+        if init == "omega":   # the kernel: separate primal and dual step lengths (update_body)
+            ap = min(1.0, eta * _max_step(s, ds, np.ones_like(lam), np.zeros_like(dl)))
+            ad = min(1.0, eta * _max_step(np.ones_like(s), np.zeros_like(ds), lam, dl))
+            x = x + ap * dx; s = s + ap * ds; lam = lam + ad * dl
+            continue
         a = min(1.0, eta * _max_step(s, ds, lam, dl))
         x = x + a * dx; s = s + a * ds; lam = lam + a * dl
     return x, s, lam, maxit, 0

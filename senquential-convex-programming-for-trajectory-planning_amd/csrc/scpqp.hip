@@ -2303,14 +2303,41 @@ __device__ __forceinline__ double affine_body(const LT& L, double mu) {
     const double sr = red[0] / L.mc / mu;
     return sr * sr * sr * mu;
 }
+// Separate primal and dual step lengths (round 3): (z, s) move by the primal ratio test
+// and lam by the dual one, each damped by step_factor.  The QP's dual residual is then no
+// longer scaled by (1 - a) exactly (P couples it to the primal step), which the next
+// iteration's residuals absorb.  CPU study, cold IPM iterations per QP: c2 11.4 -> 10.9,
+// Hp 30 11.0 -> 10.1, c3 14.0 -> 13.1 (max 23 -> 19), frog 15.9 -> 11.0; Hp 10 and
+// parallel5 unchanged; every polish certifies the same minimiser.
+#ifndef SCPQP_SPLIT_STEP
+#define SCPQP_SPLIT_STEP 1
+#endif
 template <class LT>
 __device__ __forceinline__ void update_body(const LT& L, double eta) {
+#if SCPQP_SPLIT_STEP
+    // separate step lengths: (z, s) by the primal ratio test, lam by the dual one
+    double ap = 1.0, ad = 1.0;
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        if (L.ds[r] < 0.0) ap = fmin(ap, -L.s[r] * recip(L.ds[r]));
+        if (L.dl[r] < 0.0) ad = fmin(ad, -L.lam[r] * recip(L.dl[r]));
+    }
+    double red[4] = {-ap, -ad, 0.0, 0.0};
+    block_reduce4<2>(red, 3, L.red);
+    ap = fmin(1.0, eta * -red[0]);
+    ad = fmin(1.0, eta * -red[1]);
+    for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] += ap * L.dz[e];
+    for (int r = threadIdx.x; r < L.mc; r += NT) {
+        L.s[r] += ap * L.ds[r];
+        L.lam[r] += ad * L.dl[r];
+    }
+#else
     const double alpha = fmin(1.0, eta * max_step(L));
     for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] += alpha * L.dz[e];
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         L.s[r] += alpha * L.ds[r];
         L.lam[r] += alpha * L.dl[r];
     }
+#endif
     __syncthreads();
 }
 // Fraction of the step to the boundary (round 3): max(0.99, 1 - mu) instead of a fixed

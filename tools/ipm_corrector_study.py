@@ -18,7 +18,8 @@ uses the B = 1 phase stamps of the shipped kernel (profiles/r03_phases.txt).
 
     python tools/ipm_corrector_study.py [n_problems] [c2|c3|hp10|hp30|frog|par5] [seed]
 
-The kernel's round-3 rules are "round-3 start + adaptive step" (DESIGN §3).
+The kernel's round-3 rules are "round-3 start + adaptive step + split primal / dual steps"
+(DESIGN §3).
 """
 import os
 import sys
@@ -39,7 +40,7 @@ C_CORR = 10.5e3 + 14.5e3
 
 def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, maxit=60,
         sig_pow=3, init="cvxopt", floor=1e-2, lam0=1.0, woff=1.0, shift=0.0, ulin=None, clip=0.9,
-        eta="fixed", lam_box=None, start=None):
+        eta="fixed", lam_box=None, start=None, split=False):
     mc = len(h)
     x = np.linalg.solve(P + G.T @ G, -q + G.T @ h)
     s = h - G @ x
@@ -118,7 +119,12 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
 
         dx, ds, dl = solve(s * lam)
         a = R._max_step(s, ds, lam, dl)
-        sigma = ((s + a * ds) @ (lam + a * dl) / mc / mu) ** sig_pow
+        if split == "both":   # split affine steps in the centring estimate as well
+            apa = R._max_step(s, ds, np.ones_like(lam), np.zeros_like(dl))
+            ada = R._max_step(np.ones_like(s), np.zeros_like(ds), lam, dl)
+            sigma = ((s + apa * ds) @ (lam + ada * dl) / mc / mu) ** sig_pow
+        else:
+            sigma = ((s + a * ds) @ (lam + a * dl) / mc / mu) ** sig_pow
         rc = s * lam + ds * dl - sigma * mu
         dx, ds, dl = solve(rc)
         a = R._max_step(s, ds, lam, dl)
@@ -145,6 +151,13 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
             a = min(1.0, max(eta[0], 1.0 - eta[1] * mu) * a)
         else:                        # max(0.95, 1 - 10 mu): damped further from the path
             a = min(1.0, max(0.95, 1.0 - 10 * mu) * a)
+        if split:   # separate primal (x, s) and dual (lam) step lengths
+            ap = R._max_step(s, ds, np.ones_like(lam), np.zeros_like(dl))
+            ad = R._max_step(np.ones_like(s), np.zeros_like(ds), lam, dl)
+            f = max(0.99, 1.0 - mu)
+            ap, ad = min(1.0, f * ap), min(1.0, f * ad)
+            x = x + ap * dx; s = s + ap * ds; lam = lam + ad * dl
+            continue
         x = x + a * dx; s = s + a * ds; lam = lam + a * dl
     return x, s, lam, maxit, 0, ncorr
 
@@ -198,9 +211,11 @@ def main():
     start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
     kernel = dict(start, eta="adaptive")                                   # + step_factor
     start = dict(init="omega-floor", floor=0.1, lam0=-0.3)               # ph_init_b
-    kernel = dict(start, eta="adaptive")                                   # + step_factor
+    adaptive = dict(start, eta="adaptive")                                 # + step_factor
+    kernel = dict(adaptive, split=True)                                    # + split steps
     variants = [("cvxopt start, 0.99 step (round 2)", {}), ("round-3 start, 0.99 step", start),
-                ("round-3 start + adaptive step", kernel),
+                ("round-3 start + adaptive step", adaptive),
+                ("  + split primal / dual steps (kernel)", kernel),
                 ("  + 1 Gondzio corrector", dict(kernel, K=1)), ("  + sigma^2", dict(kernel, sig_pow=2)),
                 ("  slack floor .05", dict(kernel, floor=0.05)), ("  lam0 .2", dict(kernel, lam0=-0.2)),
                 ("  box-row lam0 10", dict(kernel, lam_box=10.0)),
