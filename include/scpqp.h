@@ -76,7 +76,7 @@ typedef struct scpqp_params {
     int32_t max_ipm_iter;    /* IPM iteration cap per QP (e.g. 60)                     */
     int32_t polish_refine;   /* cap on multiplier-iteration solves per round (0: 40) */
     int32_t flags;           /* SCPQP_FLAG_* (obstacle quirk B.4 on by default)        */
-    double ipm_tol;          /* scaled KKT tolerance of the IPM (e.g. 3e-9)            */
+    double ipm_tol;          /* scaled KKT tolerance of the IPM (e.g. 1e-9)            */
     double polish_delta;     /* polish penalty delta (scaled units, default 3e-7)      */
     double polish_rho;       /* polish proximal rho (e.g. 1e-12)                       */
     const double* lf;        /* [n_veh] scenario.Lf                                    */

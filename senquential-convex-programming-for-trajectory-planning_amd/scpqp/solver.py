@@ -58,7 +58,7 @@ class ScpQpSolver:
     """Scenario-bound batched SCP-QP solver on one GPU."""
 
     def __init__(self, scenario, max_batch, device=None, hp_max=None, u_lim=None,
-                 max_scp_iter=MAX_SCP_ITER, max_ipm_iter=60, ipm_tol=3e-9, polish_delta=3e-7,
+                 max_scp_iter=MAX_SCP_ITER, max_ipm_iter=60, ipm_tol=1e-9, polish_delta=3e-7,
                  polish_rho=1e-12, polish_refine=0, obstacle_quirk=True, warm_start=True):
         if not torch.cuda.is_available():
             raise RuntimeError("scpqp: no GPU visible; the HIP path has no CPU fallback")
