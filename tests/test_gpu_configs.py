@@ -141,9 +141,10 @@ def test_c3_capped_problems_at_full_tolerance(gpu):
     """c3 problems that hit the reference's 20-QP cap (the SCP loop ends at max_scp without
     meeting its stopping rule, SCP_controller.py:40-49, 191-195; ~12 % of c3) are held to
     the same tolerances as converged ones, not exempted.  Problems 14 and 18 of the seed-0
-    stream run 20 SCP iterations in the restatement; there the restatement's own exact and
-    regularised polish modes agree to 2e-10 m over all 20 iterations, so the cap is not a
-    chaotic regime and 1e-6 m / 1e-7 rad apply."""
+    stream run 20 SCP iterations in the restatement; for these two the restatement's own exact
+    and regularised polish modes agree to 2e-10 m over all 20 iterations, so 1e-6 m / 1e-7 rad
+    apply.  (Other capped c3 problems are path-sensitive: changing the IPM tolerance moves
+    their last iterate by up to 1.2e-5 rad, profiles/r03_ab_ipm_tol_final.txt.)"""
     sc = R.circle_scenario(8, Hp=30)
     B = 24
     bt = shard.shard_batch(sc, B, 0, base_seed=0)
