@@ -154,7 +154,7 @@ def ipm(P, q, G, h, K=0, da=0.1, bmin=0.1, bmax=10.0, gamma=0.1, tol=R.IPM_TOL, 
         if split:   # separate primal (x, s) and dual (lam) step lengths
             ap = R._max_step(s, ds, np.ones_like(lam), np.zeros_like(dl))
             ad = R._max_step(np.ones_like(s), np.zeros_like(ds), lam, dl)
-            f = max(0.99, 1.0 - mu)
+            f = max(eta[0], 1.0 - eta[1] * mu) if isinstance(eta, tuple) else max(0.99, 1.0 - mu)
             ap, ad = min(1.0, f * ap), min(1.0, f * ad)
             x = x + ap * dx; s = s + ap * ds; lam = lam + ad * dl
             continue
