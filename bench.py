@@ -86,6 +86,50 @@ def cpu_baseline(bt, n_veh, sample, workers):
     return wall, cpu_s, trajs
 
 
+def pmc_traffic(tj):
+    """(corrected, raw) HBM bytes per launch from a committed traffic summary
+    (tools/pmc_summary.py): corrected = FETCH_SIZE x2 + WRITE_SIZE, raw = FETCH_SIZE +
+    WRITE_SIZE, both converted from KiB.  A summary without these keys is an error."""
+    for k in ("hbm_bytes_per_launch", "fetch_size_kib_raw", "hbm_write_bytes_per_launch"):
+        if k not in tj:
+            raise KeyError(f"traffic summary lacks {k!r}")
+    return float(tj["hbm_bytes_per_launch"]), \
+        float(tj["fetch_size_kib_raw"]) * 1024.0 + float(tj["hbm_write_bytes_per_launch"])
+
+
+def roofline_bound(sq, flops):
+    """The unit that carries the kernel's FP64 work: "mfma" when the measured MFMA
+    FLOPs (SQ_INSTS_VALU_MFMA_F64 x 2048) are at least half of the executed FLOPs,
+    else "fp64-valu" (the VALU FMA pipe; the kernel is latency-bound either way)."""
+    if not sq or not flops:
+        return "fp64-valu", "no counter record for this workload: the VALU path is assumed"
+    share = float(sq.get("mfma_f64_flops", 0.0)) / flops
+    if share >= 0.5:
+        return "mfma", f"MFMA carries {share:.0%} of the executed FP64 FLOPs"
+    return "fp64-valu", f"MFMA carries {share:.0%} of the executed FP64 FLOPs (VALU FMA pipe)"
+
+
+def cpu_leg(bt, n_veh, cpu_sample, B):
+    cores = host_cores()
+    sample = min(cpu_sample, B)
+    wall, cpu_s, cpu_trajs = cpu_baseline(bt, n_veh, sample, cores)
+    return dict(wall=wall, cpu_s=cpu_s, trajs=cpu_trajs, cores=cores, sample=sample)
+
+
+def cpu_leg_dump(cpu, path):
+    """The parent's CPU leg for the ranks it spawns (rank 0 reads it back)."""
+    d = dict(cpu, trajs=[(np.asarray(t).tolist(), int(ns), bool(cv)) for t, ns, cv in cpu["trajs"]])
+    with open(path, "w") as fh:
+        json.dump(d, fh)
+
+
+def cpu_leg_load(path):
+    with open(path) as fh:
+        d = json.load(fh)
+    d["trajs"] = [(np.asarray(t), ns, cv) for t, ns, cv in d["trajs"]]
+    return d
+
+
 def host_cores():
     try:
         n = len(os.sched_getaffinity(0))
@@ -96,7 +140,7 @@ def host_cores():
 
 
 # ----------------------------------------------------------------------------- ranks
-def spawn_ranks(n):
+def spawn_ranks(n, cpu_path=None):
     """``bench.py --gpus N`` run directly: start the N ranks as child processes of
     this one (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank r on GPU r) and
     wait for them.  Nothing here initialises the GPU (device_count() does not on
@@ -110,6 +154,8 @@ def spawn_ranks(n):
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n))
+    if cpu_path:
+        env0["SCPQP_CPU_RESULT"] = cpu_path
     ndev = torch.cuda.device_count()
     if ndev < n:
         print(f"bench: {n} ranks on {ndev} device(s): ranks share devices, gloo collectives",
@@ -160,11 +206,10 @@ def main():
         args.n_veh, args.hp, args.batch = 4, 30, args.batch if args.batch != 1024 else 3072
         mixed = (10, 20, 30)
 
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(spawn_ranks(args.gpus))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    spawner = args.gpus > 1 and "WORLD_SIZE" not in os.environ
+    world = args.gpus if spawner else int(os.environ.get("WORLD_SIZE", "1"))
+    rank = 0 if spawner else int(os.environ.get("RANK", "0"))
+    local = 0 if spawner else int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and world > 1:
         print(f"warning: WORLD_SIZE={world} != --gpus {args.gpus}", file=sys.stderr)
 
@@ -179,13 +224,30 @@ def main():
     B = args.batch
     bt = shard.shard_batch(sc, B, rank, base_seed=0, mixed_hp=mixed)
 
-    # CPU baseline first (rank 0, N=1): spawned workers, before this process touches the GPU
+    # CPU baseline first, at every N, before any process of the run touches the GPU:
+    # bench.py --gpus N run directly times it in the parent (which never initialises the
+    # GPU) on rank 0's shard and hands it to rank 0; under an external launcher rank 0
+    # times it itself before its first GPU call (the other ranks wait in the rendezvous)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cores = host_cores()
-        sample = min(args.cpu_sample, B)
-        wall, cpu_s, cpu_trajs = cpu_baseline(bt, args.n_veh, sample, cores)
-        cpu = dict(wall=wall, cpu_s=cpu_s, trajs=cpu_trajs, cores=cores, sample=sample)
+    if spawner:
+        path = None
+        if not args.no_cpu:
+            import tempfile
+            cpu = cpu_leg(bt, args.n_veh, args.cpu_sample, B)
+            fd, path = tempfile.mkstemp(prefix="scpqp_cpu_", suffix=".json")
+            os.close(fd)
+            cpu_leg_dump(cpu, path)
+        try:
+            rc = spawn_ranks(args.gpus, path)
+        finally:
+            if path:
+                os.unlink(path)
+        sys.exit(rc)
+    if rank == 0 and not args.no_cpu:
+        if os.environ.get("SCPQP_CPU_RESULT"):
+            cpu = cpu_leg_load(os.environ["SCPQP_CPU_RESULT"])
+        else:
+            cpu = cpu_leg(bt, args.n_veh, args.cpu_sample, B)
 
     import torch
     if world > 1:
@@ -276,10 +338,10 @@ def main():
         try:
             with open(tpath) as fh:
                 tj = json.load(fh)
-            traffic = tj.get("hbm_bytes_per_launch")
-            traffic_raw = tj.get("fetch_size_bytes_raw", 0.0) + tj.get("hbm_write_bytes_per_launch", 0.0)
         except (OSError, ValueError):
-            traffic = None
+            tj = None
+        if tj is not None:
+            traffic, traffic_raw = pmc_traffic(tj)
     if B == default_b and os.path.exists(spath):
         try:
             with open(spath) as fh:
@@ -287,6 +349,7 @@ def main():
         except (OSError, ValueError):
             sq = None
     res = S.resources()
+    bound, bound_note = roofline_bound(sq, flops)
 
     line = {
         "metric": METRIC,
@@ -308,14 +371,14 @@ def main():
                    "parallelism": (f"{world} of 8 shards of c4's 65536 problems (8192 per rank, "
                                    f"no collective)" if args.config == "c4" else
                                    f"{world} independent shards (no collective)")},
-        "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
+        "roofline": {"bound": bound, "bound_note": bound_note, "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "kernel": "scp_kernel", "kernel_ms": kern_ms,
                      "traffic_source": f"profiles/{os.path.basename(tpath)} (FETCH_SIZE x2 + WRITE_SIZE)"
                      if traffic is not None else None,
                      "traffic_raw_fetch": traffic_raw,
-                     "traffic_raw_note": "raw FETCH_SIZE + WRITE_SIZE (no x2 read correction; the true HBM "
-                                         "bytes lie between traffic_raw_fetch and traffic)"
+                     "traffic_raw_note": "raw FETCH_SIZE + WRITE_SIZE in bytes (no x2 read correction; "
+                                         "the true HBM bytes lie between traffic_raw_fetch and traffic)"
                      if traffic_raw is not None else None,
                      "hbm_achieved_GBps": traffic / (kern_ms * 1e-3) / 1e9 if traffic else None,
                      "hbm_frac": traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if traffic else None,

@@ -112,7 +112,8 @@ def test_bench_spawns_ranks_itself(gpu):
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT",
                         "SCPQP_DIST_BACKEND")}
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--no-cpu", "--batch", "256"]
+           "--warmup", "1", "--cpu-sample", "4", "--batch", "256"]
+    env["SCPQP_CPU_WORKERS"] = "2"
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
@@ -120,3 +121,6 @@ def test_bench_spawns_ranks_itself(gpu):
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["batch_per_gpu"] == 256
     assert d["value"] == pytest.approx(2 * 256 * 2 / (d["ms_per_step"] * 2 * 1e-3), rel=1e-9)
+    # the CPU leg runs in the launching process before the ranks start, at every N
+    assert d["cpu_baseline"]["cores"] == 2 and d["cpu_baseline"]["value"] > 0
+    assert d["traj_linf_err"] is not None and d["traj_linf_err"] < 1e-6

@@ -6,6 +6,8 @@ model); every solve/linearise/evaluate/sample call needs the GPU and lives in
 the -m gpu tests.
 """
 import math
+import os
+import sys
 
 import numpy as np
 import pytest
@@ -167,3 +169,44 @@ def test_config_and_miqp_stub():
     assert Config.Config().QCQP.constraintTolerance == pytest.approx(0.0042)
     with pytest.raises(NotImplementedError):
         MIQP.MIQPcontroller(None, None, None)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_bench_traffic_and_bound_from_committed_records():
+    """bench.py reads the committed PMC summaries: raw = FETCH_SIZE (KiB) + WRITE_SIZE,
+    corrected = 2 FETCH_SIZE + WRITE_SIZE; the roofline bound follows the measured MFMA
+    share (the raw key and the hard-coded "mfma" label were wrong)."""
+    import glob
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0[3-9]_pmc_traffic_c*.json")))
+    assert paths
+    for path in paths:
+        with open(path) as fh:
+            tj = json.load(fh)
+        corr, raw = bench.pmc_traffic(tj)
+        assert raw == pytest.approx(tj["fetch_size_kib_raw"] * 1024 + tj["write_size_kib"] * 1024)
+        assert corr == pytest.approx(2 * tj["fetch_size_kib_raw"] * 1024 + tj["write_size_kib"] * 1024)
+        assert raw < corr
+    with pytest.raises(KeyError):
+        bench.pmc_traffic({"hbm_bytes_per_launch": 1.0})
+    assert bench.roofline_bound({"mfma_f64_flops": 0.0}, 1e9)[0] == "fp64-valu"
+    assert bench.roofline_bound({"mfma_f64_flops": 0.6e9}, 1e9)[0] == "mfma"
+    assert bench.roofline_bound(None, 1e9)[0] == "fp64-valu"
+
+
+def test_bench_cpu_leg_round_trip(tmp_path):
+    """The CPU leg the launching process hands to rank 0 survives the JSON round trip."""
+    sys.path.insert(0, ROOT)
+    import bench
+    cpu = dict(wall=1.5, cpu_s=3.0, cores=2, sample=2,
+               trajs=[(np.arange(6.0).reshape(3, 2), 5, True), (np.ones((3, 2)), 20, False)])
+    path = str(tmp_path / "cpu.json")
+    bench.cpu_leg_dump(cpu, path)
+    back = bench.cpu_leg_load(path)
+    assert back["wall"] == 1.5 and back["cores"] == 2 and back["sample"] == 2
+    for (t0, n0, c0), (t1, n1, c1) in zip(cpu["trajs"], back["trajs"]):
+        assert np.array_equal(t0, t1) and n0 == n1 and c0 == c1

@@ -284,8 +284,94 @@ def study_blocktri(nprob=8, bs=8, nveh=4, hp=20):
               f"|x - exact| max {np.nanmax(e):.2e}")
 
 
+# ---------------------------------------------------------------------------------
+# Variant 3 (round 4): keep L D L' and invert the unit-lower factor explicitly
+# (block rows of L^-1 by forward substitution, as the device's helper waves would
+# form them beside the panel chain); every solve is then two triangular mat-vecs,
+# x = L^-T (D^-1 (L^-1 r)), with no substitution chain.
+class LinvTri:
+    def __init__(self, K, bs=8):
+        import scipy.linalg
+        self.L, self.D = ldl(K)
+        n = K.shape[0]
+        X = np.zeros((n, n))
+        for a in range(0, n, bs):   # block row a of X = L^-1
+            b = min(n, a + bs)
+            Li = scipy.linalg.solve_triangular(self.L[a:b, a:b], np.eye(b - a), lower=True,
+                                               unit_diagonal=True)
+            rhs = -self.L[a:b, :a] @ X[:a, :a]
+            X[a:b, :a] = Li @ rhs
+            X[a:b, a:b] = Li
+        self.X = X
+
+    def solve(self, r):
+        y = self.X @ r
+        return self.X.T @ (y / self.D)
+
+
+def study_linv(nprob=8, bs=8, nveh=4, hp=20):
+    global Inv
+    base_inv = Inv
+
+    class InvL(base_inv):
+        def __init__(self, K, mode, blk):
+            self.mode = mode
+            if mode == "chol":
+                return base_inv.__init__(self, K, mode, blk)
+            self.T = LinvTri(K, bs)
+            self.K = K
+
+        def solve(self, r):
+            if self.mode == "chol":
+                return base_inv.solve(self, r)
+            x = self.T.solve(r)
+            if self.mode == "linv+ir":
+                x = x + self.T.solve(r - self.K @ x)
+            return x
+
+    Inv = InvL
+    sc = R.circle_scenario(nveh, Hp=hp)
+    bt = BT.make_batch(sc, nprob, base_seed=77)
+    N = nveh * hp
+    stats = {m: dict(it=[], fail=0, pol=0, nsol=[], err=[]) for m in ("chol", "linv", "linv+ir")}
+    for b in range(nprob):
+        p = R.make_problem(sc, bt.x0[b], bt.u0[b], bt.ec_noise[b], Hp=hp)
+        r = R.scp_solve(p, mode="structured", keep_history=True)
+        lin = R.linearise(p, "structured")
+        Phi0 = np.zeros((N, N)); Psi0 = np.zeros(N)
+        for v in range(nveh):
+            Phi0[hp * v:hp * (v + 1), hp * v:hp * (v + 1)] = lin.Phi0[v]
+            Psi0[hp * v:hp * (v + 1)] = lin.Psi0[v]
+        for hh in r.history:
+            P, q, G, h = R.qp_matrices(Phi0, Psi0, hh["A"], hh["b"], p.u_lim)
+            Ps, qs, Gs, hs, sv, rn = R.qp_scale(P, q, G, h, p.u_lim, N)
+            ref = R.qp_polish_exact(Ps, qs, Gs, hs, *R.qp_ipm(Ps, qs, Gs, hs)[:3])
+            for m, st in stats.items():
+                x, s, lam, it, code = ipm(Ps, qs, Gs, hs, m, 4)
+                st["it"].append(it)
+                st["fail"] += code != 1
+                pol = polish(Ps, qs, Gs, hs, x, s, lam, m, 4)
+                if pol is not None:
+                    st["pol"] += 1
+                    st["nsol"].append(pol[2])
+                    if ref is not None:
+                        st["err"].append(float(np.abs(pol[0] - ref[0]).max()))
+    Inv = base_inv
+    nqp = len(stats["chol"]["it"])
+    print(f"explicit L^-1 solves, block {bs}: {nprob} problems, {nqp} QPs (nveh {nveh}, Hp {hp})")
+    for m, st in stats.items():
+        e = np.array(st["err"]) if st["err"] else np.array([np.nan])
+        print(f"  {m:8s}: IPM its mean {np.mean(st['it']):.2f} max {max(st['it'])}, not converged "
+              f"{st['fail']}, polish certified {st['pol']}/{nqp}, solves/QP {np.mean(st['nsol']):.2f}, "
+              f"|x - exact| max {np.nanmax(e):.2e}")
+
+
 if __name__ == "__main__":
-    if len(sys.argv) > 1 and sys.argv[1] == "blocktri":
+    if len(sys.argv) > 1 and sys.argv[1] == "linv":
+        study_linv(int(sys.argv[2]) if len(sys.argv) > 2 else 8, 8,
+                   int(sys.argv[3]) if len(sys.argv) > 3 else 4,
+                   int(sys.argv[4]) if len(sys.argv) > 4 else 20)
+    elif len(sys.argv) > 1 and sys.argv[1] == "blocktri":
         study_blocktri(int(sys.argv[2]) if len(sys.argv) > 2 else 8,
                        int(sys.argv[3]) if len(sys.argv) > 3 else 8)
     else:
