@@ -13,15 +13,18 @@ What differs from the reference, on purpose:
 * the QP backend is the kernel's interior point method + active-set polish
   instead of cvxpy/GUROBI (the QP is strictly convex, so the minimiser is the
   same to solver tolerance; see DESIGN.md);
-* ``optimization_log`` holds the reference's per-iteration lists
-  (SCP_controller.py:169-189: 'Aineq', 'bineq', 'x', 'slack', 'QCQP_ObjVal',
-  'SCP_ObjVal', 'delta', 'u', 'prev_u', 'feasible'), rebuilt from the kernel's
-  per-iteration trace, plus per-solve counters (SCP/IPM iterations, status
-  flags).  The lists are decoded on first access (``_LazyLog``): main.py never
-  reads the log, so the device-to-host copy of the trace and the dense row
-  rebuild stay out of ``optimizerTime``.  'P', 'q', 'lb', 'ub' are the same
-  every iteration and are not repeated; the forward_U trajectories of the log
-  are not rebuilt;
+* ``optimization_log`` holds every per-iteration list of the reference
+  (SCP_controller.py:88-90, 169-189: 'P', 'q', 'Aineq', 'bineq', 'lb', 'ub',
+  'x', 'slack', 'SCP_ObjVal', 'QCQP_ObjVal', 'delta_hat', 'delta', 'u',
+  'feasible', 'prev_u', 'Traj', 'U', 'prevTraj', 'prevU'), rebuilt from the
+  kernel's per-iteration trace, plus per-solve counters (SCP/IPM iterations,
+  status flags).  The trace rows of the solve are copied to the host with the
+  result; the lists are decoded from them on first access (``_LazyLog``), so
+  the dense row rebuild stays out of ``optimizerTime``.  The decode holds host
+  arrays only (no controller, no device tensors): a log can be copied or
+  pickled (the copy is the decoded plain dict).  'Traj'/'prevTraj' are the
+  predicted positions ``const_term + Mathcal_B u`` of forward_U, evaluated on
+  the host from the same linearisation;
 * the dense ``qcqp`` dictionary (QCQP_formulate, SCP_controller.py:278-341) is
   built lazily, only if a caller reads ``.qcqp``; the solve uses the
   factored forms on the device.
@@ -29,6 +32,7 @@ What differs from the reference, on purpose:
   (SCP_controller.py:51-66) builds an (n x n) warm start and cannot run
   (SURVEY B.9); here the result is flagged ``resultInvalid``.
 """
+import functools
 import time
 
 import numpy as np
@@ -42,12 +46,47 @@ ST_INVALID = 2      # SCPQP_ST_INVALID
 
 
 class _LazyLog(dict):
-    """optimization_log whose per-iteration lists are decoded from the device trace
-    the first time any key beyond the counters is read (or the log is iterated)."""
+    """optimization_log whose per-iteration lists are decoded from the host copy of
+    the device trace the first time any key beyond the counters is read (or the log is
+    iterated, copied, compared, printed or pickled)."""
 
     def __init__(self, counters, decode):
         super().__init__(counters)
         self._decode = decode
+
+    def copy(self):
+        self._fill()
+        return dict(self)
+
+    def __reduce__(self):
+        self._fill()
+        return (dict, (dict(self),))
+
+    def __repr__(self):
+        self._fill()
+        return super().__repr__()
+
+    def __eq__(self, other):
+        self._fill()
+        return super().__eq__(other)
+
+    __hash__ = None
+
+    def pop(self, k, *default):
+        self._fill()
+        return super().pop(k, *default)
+
+    def popitem(self):
+        self._fill()
+        return super().popitem()
+
+    def setdefault(self, k, default=None):
+        self._fill()
+        return super().setdefault(k, default)
+
+    def update(self, *a, **kw):
+        self._fill()
+        return super().update(*a, **kw)
 
     def _fill(self):
         if self._decode is not None:
@@ -86,6 +125,77 @@ class _LazyLog(dict):
     def values(self):
         self._fill()
         return super().values()
+
+
+SLACK_WEIGHT = 1e5          # psi_omega_weight, SCP_controller.py:84
+OMEGA_UB = 1e25             # upper_bound_omega, SCP_controller.py:85
+
+
+def _iteration_log(trace, n_scp, nV, nO, Hp, hp_max, u_lim, Mb, const_term, Phi_0, Psi_0,
+                   gamma0):
+    """The reference's per-iteration optimization_log lists (SCP_controller.py:88-90,
+    169-189) from the host copy of one problem's device trace.
+    * P = blkdiag(2 Phi0, 0), q = [Psi0; 1e5], lb = [-uLim; 0], ub = [uLim; 1e25]
+      (:117-127; the same arrays every iteration, as the reference appends them);
+    * Aineq / bineq: dense rows from the factored ones and the Toeplitz blocks (:93-128);
+    * x = [u; slack], SCP_ObjVal = fval = 1/2 x'Px + q'x + gamma0 (:146, :158);
+    * delta_hat = (obj_0 + 1e5 maxviol_0) - fval (:159), where obj_0 + 1e5 maxviol_0 is
+      the previous evaluation's, recovered from the recorded delta = that - (obj + 1e5
+      maxviol) (:160);
+    * Traj / U, prevTraj / prevU: forward_U of u and of the linearisation point (:183-187):
+      positions const_term + Mathcal_B u, U = u per vehicle [Hp, nu, nVeh]."""
+    from scpqp import trace as TR
+    N = nV * Hp
+    g = np.stack([Mb[0::2, 0, v] for v in range(nV)], 0)        # g_k x-components
+    g = np.stack([g, np.stack([Mb[1::2, 0, v] for v in range(nV)], 0)], -1)
+    its = TR.decode(trace, n_scp, nV, nO, Hp, hp_max, g=g, u_lim=u_lim)
+    Phi0 = np.zeros((N, N))
+    Psi0 = np.zeros(N)
+    for v in range(nV):
+        sl = slice(v * Hp, (v + 1) * Hp)
+        Phi0[sl, sl] = Phi_0[:, :, v]
+        Psi0[sl] = Psi_0[:, 0, v]
+    P = np.zeros((N + 1, N + 1))
+    P[:N, :N] = 2 * Phi0
+    q = np.vstack([Psi0.reshape(-1, 1), [[SLACK_WEIGHT]]])
+    lb = np.vstack([-np.ones((N, 1)) * u_lim, [[0.0]]])
+    ub = np.vstack([np.ones((N, 1)) * u_lim, [[OMEGA_UB]]])
+
+    def forward_U(uu):
+        U = uu.reshape(nV, Hp).T[:, None, :].copy()                # [Hp, nu, nVeh]
+        traj = np.stack([const_term[:, 0, v] + Mb[:, :, v] @ uu[v * Hp:(v + 1) * Hp]
+                         for v in range(nV)], -1).reshape(Hp, 2, nV)
+        return traj, U
+
+    log = {k: [] for k in ('P', 'q', 'Aineq', 'bineq', 'lb', 'ub', 'x', 'slack', 'SCP_ObjVal',
+                           'QCQP_ObjVal', 'delta_hat', 'delta', 'u', 'feasible', 'prev_u', 'Traj',
+                           'U', 'prevTraj', 'prevU', 'ipm_iters')}
+    for d in its:
+        uu = d['z'][:-1]
+        fval = float(uu @ Phi0 @ uu + Psi0 @ uu + SLACK_WEIGHT * d['slack'] + gamma0)
+        prev_merit = d['delta'] + d['obj'] + SLACK_WEIGHT * d['maxviol']
+        log['P'].append(P)
+        log['q'].append(q)
+        log['Aineq'].append(d['A'])
+        log['bineq'].append(d['b'].reshape(-1, 1))
+        log['lb'].append(lb)
+        log['ub'].append(ub)
+        log['x'].append(d['z'].reshape(-1, 1))
+        log['slack'].append(d['slack'])
+        log['SCP_ObjVal'].append(fval)
+        log['QCQP_ObjVal'].append(np.array([[d['obj']]]))
+        log['delta_hat'].append(prev_merit - fval)
+        log['delta'].append(d['delta'])
+        log['u'].append(uu.reshape(-1, 1))
+        log['feasible'].append(d['feasible'])
+        log['prev_u'].append(d['u_lin'].reshape(-1, 1))
+        for key, vec in (('', uu), ('prev', d['u_lin'])):
+            traj, U = forward_U(vec)
+            log[key + 'Traj'].append(traj)
+            log[key + 'U'].append(U)
+        log['ipm_iters'].append(d['ipm_iters'])
+    log['trace'] = its          # decoded kernel records (max_violation per iteration, rows)
+    return log
 
 
 class SCPcontroller:
@@ -143,50 +253,21 @@ class SCPcontroller:
                                 **self._inputs())
         u = res.u[0, :self.nVeh * self.Hp].cpu().numpy().reshape(-1, 1)
         status = int(res.status[0].item())
+        n_scp = int(res.n_scp[0].item())
+        m = self.mpc
+        # the decode's inputs, host arrays only (the trace rows of this solve and the
+        # linearisation): the log keeps neither the controller nor device tensors alive
+        dec = functools.partial(_iteration_log, res.trace[0, :n_scp].cpu().numpy(), n_scp,
+                                self.nVeh, self.nObst, self.Hp, self.solver.hp_max,
+                                self.scenario_uLim, m.Mathcal_B.copy(), m.const_term.copy(),
+                                m.Phi_0.copy(), m.Psi_0.copy(), float(np.sum(m.gamma_0)))
         log = _LazyLog({'status': status & 0xff, 'flags': status & ~0xff,
-                        'n_scp': int(res.n_scp[0].item()), 'n_ipm': int(res.n_ipm[0].item()),
+                        'n_scp': n_scp, 'n_ipm': int(res.n_ipm[0].item()),
                         'obj': float(res.obj[0].item()),
                         'max_violation': float(res.max_violation[0].item()),
-                        'sum_violations': float(res.sum_violations[0].item())},
-                       lambda: self._iteration_log(res))
+                        'sum_violations': float(res.sum_violations[0].item())}, dec)
         self._last_traj = res.traj[0, :self.Hp].cpu().numpy()
         return u, bool(res.feasible[0].item()), float(res.obj[0].item()), log
-
-    def _iteration_log(self, res):
-        """The reference's per-iteration optimization_log lists (SCP_controller.py:169-189)
-        from the device trace: dense Aineq/bineq from the factored rows and the
-        Toeplitz blocks, x = [u; slack], SCP_ObjVal = 1/2 x'Px + q'x + gamma0."""
-        from scpqp import trace as TR
-        nV, Hp, nO = self.nVeh, self.Hp, self.nObst
-        m = self.mpc
-        g = np.stack([m.Mathcal_B[0::2, 0, v] for v in range(nV)], 0)        # g_k x-components
-        g = np.stack([g, np.stack([m.Mathcal_B[1::2, 0, v] for v in range(nV)], 0)], -1)
-        its = TR.decode(res.trace[0].cpu().numpy(), int(res.n_scp[0].item()), nV, nO, Hp,
-                        self.solver.hp_max, g=g, u_lim=self.scenario_uLim)
-        Phi0 = np.zeros((nV * Hp, nV * Hp))
-        Psi0 = np.zeros(nV * Hp)
-        for v in range(nV):
-            sl = slice(v * Hp, (v + 1) * Hp)
-            Phi0[sl, sl] = m.Phi_0[:, :, v]
-            Psi0[sl] = m.Psi_0[:, 0, v]
-        gamma0 = float(np.sum(m.gamma_0))
-        log = {k: [] for k in ('Aineq', 'bineq', 'x', 'slack', 'SCP_ObjVal', 'QCQP_ObjVal',
-                               'delta', 'u', 'feasible', 'prev_u', 'ipm_iters')}
-        for d in its:
-            uu = d['z'][:-1]
-            log['Aineq'].append(d['A'])
-            log['bineq'].append(d['b'].reshape(-1, 1))
-            log['x'].append(d['z'].reshape(-1, 1))
-            log['slack'].append(d['slack'])
-            log['SCP_ObjVal'].append(float(uu @ Phi0 @ uu + Psi0 @ uu + 1e5 * d['slack'] + gamma0))
-            log['QCQP_ObjVal'].append(np.array([[d['obj']]]))
-            log['delta'].append(d['delta'])
-            log['u'].append(uu.reshape(-1, 1))
-            log['feasible'].append(d['feasible'])
-            log['prev_u'].append(d['u_lin'].reshape(-1, 1))
-            log['ipm_iters'].append(d['ipm_iters'])
-        log['trace'] = its          # decoded kernel records (max_violation per iteration, rows)
-        return log
 
     # ------------------------------------------------------------------ SCP_controller.py:199-213
     def forward_U(self, u):

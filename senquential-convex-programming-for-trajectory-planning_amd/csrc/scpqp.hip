@@ -2737,7 +2737,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     PROF_ACC(16);
     // ---- Mehrotra iterations
     int it = 0;
-    bool conv = false, ok = false;
+    bool conv = false, ok = false, maxit = false;
     double tol = K.ipmTol;
     D4 res = PH(ph_residuals)(c);
     PROF_ACC(1);
@@ -2774,6 +2774,9 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
             PROF_ACC(6);
 #endif
         }
+        // the iteration cap counts against the QP only in the first pass: a resumed pass
+        // (below) runs 100x tighter than the QP's tolerance, which it has already met
+        if (pass == 0 && !conv && it >= K.maxIpm) maxit = true;
         // ---- active-set polish on {lam > s}
         PH(ph_polish_prep)(c);
         ok = polish_rounds<HG, VG, RM, OCC, SH>(c, hmax, K.polRho, kPolishRounds, K.nRefine, INFINITY, st);
@@ -2789,7 +2792,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
         res = PH(ph_residuals)(c);
     }
     st.ipm += it;
-    if (!conv && it >= K.maxIpm) qflags |= SCPQP_FL_IPM_MAXIT;
+    if (maxit) qflags |= SCPQP_FL_IPM_MAXIT;
     if (!ok) qflags |= SCPQP_FL_POLISH_REJECTED;
     return ok;
 }

@@ -210,3 +210,73 @@ def test_bench_cpu_leg_round_trip(tmp_path):
     assert back["wall"] == 1.5 and back["cores"] == 2 and back["sample"] == 2
     for (t0, n0, c0), (t1, n1, c1) in zip(cpu["trajs"], back["trajs"]):
         assert np.array_equal(t0, t1) and n0 == n1 and c0 == c1
+
+
+def _lazy_log_counter():
+    calls = []
+
+    def dec():
+        calls.append(1)
+        return {"x": [np.ones((3, 1))], "delta": [0.5]}
+    return calls, dec
+
+
+def test_lazy_log_copy_and_pickle_decode_first():
+    """optimization_log: copy / pickle / pop see the decoded lists, and the
+    decode runs once."""
+    import copy
+    import pickle
+    import SCP_controller as SC
+    calls, dec = _lazy_log_counter()
+    log = SC._LazyLog({"status": 0, "n_scp": 1}, dec)
+    assert dict.__contains__(log, "status") and not calls
+    c = log.copy()
+    assert c["delta"] == [0.5] and len(calls) == 1
+    back = pickle.loads(pickle.dumps(log))
+    assert back["x"][0].shape == (3, 1) and back["status"] == 0
+    assert copy.copy(log)["delta"] == [0.5] and copy.deepcopy(log)["n_scp"] == 1
+    assert log.pop("delta") == [0.5] and len(calls) == 1
+
+
+def test_iteration_log_keys_and_formulas():
+    """The drop-in's per-iteration log has every key of SCP_controller.py:88-90 with the
+    reference's shapes; delta_hat, fval and forward_U follow their formulas (:146-187)."""
+    import SCP_controller as SC
+    from scpqp import trace as TR
+    rng = np.random.default_rng(3)
+    nV, nO, Hp, u_lim = 3, 1, 5, 0.4
+    N = nV * Hp
+    m = len(TR.row_list(nV, Hp, nO))
+    stride = TR.HDR + 2 * N + 4 * m
+    n_scp = 2
+    tr = rng.standard_normal((n_scp, stride))
+    tr[:, 5] = 7.0                       # ipm iterations
+    tr[:, 6] = 1.0
+    tr[:, 7] = 1.0
+    tr[:, TR.HDR + 2 * N + 2::4] = -np.abs(tr[:, TR.HDR + 2 * N + 2::4]) - 0.5   # w_r < 0
+    Mb = rng.standard_normal((2 * Hp, Hp, nV))
+    const_term = rng.standard_normal((2 * Hp, 1, nV))
+    Phi_0 = np.stack([np.eye(Hp) * (v + 1) for v in range(nV)], -1)
+    Psi_0 = rng.standard_normal((Hp, 1, nV))
+    log = SC._iteration_log(tr, n_scp, nV, nO, Hp, Hp, u_lim, Mb, const_term, Phi_0, Psi_0, 2.5)
+    for k in ("P", "q", "Aineq", "bineq", "lb", "ub", "x", "slack", "SCP_ObjVal", "QCQP_ObjVal",
+              "delta_hat", "delta", "u", "feasible", "prev_u", "Traj", "U", "prevTraj", "prevU"):
+        assert len(log[k]) == n_scp, k
+    assert log["P"][0].shape == (N + 1, N + 1) and log["P"][0][N, N] == 0.0
+    assert log["q"][0][-1, 0] == 1e5 and log["ub"][0][-1, 0] == 1e25 and log["lb"][0][-1, 0] == 0
+    assert np.all(log["ub"][0][:N] == u_lim) and np.all(log["lb"][0][:N] == -u_lim)
+    assert log["Aineq"][0].shape == (m, N + 1) and log["Traj"][0].shape == (Hp, 2, nV)
+    assert log["U"][0].shape == (Hp, 1, nV)
+    for it in range(n_scp):
+        x = log["x"][it].reshape(-1)
+        fval = 0.5 * x @ log["P"][it] @ x + log["q"][it].reshape(-1) @ x + 2.5
+        assert log["SCP_ObjVal"][it] == pytest.approx(fval, rel=1e-12)
+        merit = tr[it, 0] + tr[it, 1] + 1e5 * tr[it, 2]
+        assert log["delta_hat"][it] == pytest.approx(merit - fval, rel=1e-12)
+        u = log["u"][it].reshape(-1)
+        for v in range(nV):
+            X = (const_term[:, :, v] + Mb[:, :, v] @ u[v * Hp:(v + 1) * Hp, None]).reshape(2, Hp, order="F")
+            assert np.allclose(log["Traj"][it][:, :, v], X.T)
+            assert np.allclose(log["U"][it][:, 0, v], u[v * Hp:(v + 1) * Hp])
+        pu = log["prev_u"][it].reshape(-1)
+        assert np.allclose(log["prevU"][it][:, 0, 0], pu[:Hp])
