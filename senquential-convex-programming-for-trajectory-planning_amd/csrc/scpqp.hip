@@ -45,10 +45,7 @@
 
 #include "scpqp.h"
 
-#ifndef SCPQP_NT
-#define SCPQP_NT 256
-#endif
-#define NT SCPQP_NT
+#define NT 256            // threads per workgroup (4 wave64)
 #define TXD 16            // column stride of the 2-D thread grid
 #define TYD (NT / TXD)    // row stride
 #define NWAVE (NT / 64)
@@ -942,9 +939,6 @@ __device__ double gt_apply(const LT& L, PT t, PO out) {
 // own lower summation bound.  A tile's cost is its trip count Hb - TS max(lt, mt):
 // tiles are enumerated by decreasing cost and dealt to the threads in snake
 // order, so every thread gets about the same number of trips.
-#ifndef SCPQP_ASM_PREFETCH
-#define SCPQP_ASM_PREFETCH 1
-#endif
 template <int TS, class LT, class PD>
 __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD d, double rho) {
     const int tid = threadIdx.x, V = L.V, Hb = L.Hb, nb = L.nb, N = L.N;
@@ -974,7 +968,6 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
         for (int i = 0; i < TS; ++i)
 #pragma unroll
             for (int j = 0; j < TS; ++j) c[i][j] = 0.0;
-#if SCPQP_ASM_PREFETCH
         // software pipeline: the next step's g and W~ loads are in flight while this
         // step's products run (the loop is LDS-latency-bound, not FMA-bound)
         double2v an = ld2(ga + 2 * (k0 - l0)), bn = ld2(gb + 2 * (k0 - m0));
@@ -982,7 +975,7 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
         // two steps ahead where g / W~ come from the workspace (plan 2: c3 5.36k -> 5.54k
         // solves/s, profiles/r03_ab_prefetch.txt); one step for the LDS plans (c2, c5:
         // within noise or slower)
-        constexpr bool PF2 = SCPQP_ASM_PREFETCH >= 2 || LT::HGLOBAL;
+        constexpr bool PF2 = LT::HGLOBAL;
         double2v an2 = an, bn2 = bn, wm0 = wn0, wm1 = wn1;
         if constexpr (PF2) {
             const int k1 = k0 + 1 < Hb ? k0 + 1 : k0;
@@ -1017,26 +1010,6 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
                 wn0 = ld2(W + 4 * kn * nb);
                 wn1 = ld2(W + 4 * kn * nb + 2);
             }
-#else
-        for (int k = k0; k < Hb; ++k) {
-            if constexpr (TS == 2) {
-                // 2 x 2 (c2): reloading the second row / column measured ~1 % faster
-                // than the sliding window (profiles/r02_ab_assembly.txt)
-                av[0] = ld2(ga + 2 * (k - l0));
-                bv[0] = ld2(gb + 2 * (k - m0));
-                av[1] = k > l0 ? ld2(ga + 2 * (k - l0 - 1)) : zero2;
-                bv[1] = k > m0 ? ld2(gb + 2 * (k - m0 - 1)) : zero2;
-            } else {
-#pragma unroll
-                for (int i = TS - 1; i > 0; --i) {
-                    av[i] = av[i - 1];
-                    bv[i] = bv[i - 1];
-                }
-                av[0] = ld2(ga + 2 * (k - l0));
-                bv[0] = ld2(gb + 2 * (k - m0));
-            }
-            const double2v w0 = ld2(W + 4 * k * nb), w1 = ld2(W + 4 * k * nb + 2);
-#endif
             double px[TS], py[TS];   // W~ g_b for every column
 #pragma unroll
             for (int j = 0; j < TS; ++j) {
@@ -1153,14 +1126,7 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
 // double-buffered by panel parity.  Returns false on a non-positive pivot
 // (K not numerically positive definite).
 // ---------------------------------------------------------------------------
-#ifndef SCPQP_CB
-#define SCPQP_CB 8
-#endif
-#define CB SCPQP_CB
-#ifndef SCPQP_PANEL2
-#define SCPQP_PANEL2 1
-#endif
-static_assert(CB % 4 == 0 && CB <= 8, "panel width");
+#define CB 8   // panel width (4 measured slower: DESIGN §3)
 
 // 1/x for a positive finite pivot: v_rcp_f64 + two Newton steps (full precision,
 // a fraction of the IEEE division sequence's latency on the serial panel path).
@@ -1192,8 +1158,13 @@ __device__ __forceinline__ bool is_lead(int lead) { return wave_id() == lead; }
 __device__ __forceinline__ void lead_prio_up() { __builtin_amdgcn_s_setprio(2); }
 __device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0); }
 
-// Panel factorisation, round-3 form (SCPQP_PANEL2).  Same algorithm and operands as
-// panel_factor below, restructured to shorten the lead's dependency chain:
+// Panel factorisation (the lead wave): the panel of columns [r0, r0 + jb) in registers,
+// rows i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB update of
+// the previous panel(s) (columns [jp, jp + nprev CB), pivots dprev).  Branch-free: rows
+// >= n read a clamped row, columns >= jb of the last panel are padded with an identity
+// block (D = 1, no coupling), and entries above the diagonal (lane < c) only hold values
+// that are never broadcast or stored.  Round-3 form; its chain is shorter than the
+// column-by-column form's (two v_readlane round trips per pivot column):
 //  * look-ahead from the most recent panel: its D-scaled rows r0 .. r0 + 7 were left in
 //    LDS (ldbuf, 8 x 8) by the previous step's lead, so they are read as broadcast
 //    loads instead of 64 v_readlane pairs; an older panel (grouped trailing update)
@@ -1205,7 +1176,7 @@ __device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0)
 //    (p_ic -= (p_ic' / D_c') U_cc', U = L D unscaled), which for the block's own rows
 //    repeats the uniform factorisation operation for operation.
 template <int RS, class HP>
-__device__ __forceinline__ void panel_factor2(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
+__device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
                                               const ldouble* dprev, ldouble* dout, lint* flag,
                                               int nprev, ldouble* ldbuf) {
     const int lane = threadIdx.x & 63;
@@ -1350,114 +1321,6 @@ __device__ __forceinline__ void panel_factor2(HP H, ldouble* dinv, int n, int r0
     PROF_ACC_FINE(21);
 }
 
-// Wave 0: factor the panel of columns [r0, r0 + jb) in registers, rows
-// i = r0 + lane + 64 t.  If jp >= 0 the panel first receives the rank-CB
-// update of the previous panel (columns [jp, jp + CB), pivots dprev).
-// Branch-free: rows >= n read a clamped row, columns >= jb of the last panel
-// are padded with an identity block (D = 1, no coupling), and entries above
-// the diagonal (lane < c) only hold values that are never broadcast or stored.
-template <int RS, class HP>
-__device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
-                                             const ldouble* dprev, ldouble* dout, lint* flag,
-                                             int nprev, ldouble* ldbuf) {
-#if SCPQP_PANEL2
-    panel_factor2<RS>(H, dinv, n, r0, jb, jp, dprev, dout, flag, nprev, ldbuf);
-    return;
-#endif
-    (void)ldbuf;
-    const int lane = threadIdx.x & 63;
-    PROF_T0_FINE();
-    double p[RS][CB];
-    int ro[RS];
-#pragma unroll
-    for (int t = 0; t < RS; ++t) {
-        const int i = r0 + lane + 64 * t;
-        ro[t] = roff(i < n ? i : n - 1);
-#pragma unroll
-        for (int c = 0; c < CB; c += 2) {
-            const double2v v = ld2(H + ro[t] + r0 + c);
-            p[t][c] = v.x;
-            p[t][c + 1] = v.y;
-        }
-    }
-#ifdef SCPQP_PROF_FINE
-    __builtin_amdgcn_s_waitcnt(0);
-#endif
-    PROF_ACC_FINE(18);
-    // look-ahead update p_ic -= sum_c' L_ic' (D_c' L_{r0+c, c'}) from the nprev
-    // panels starting at column jp (two when the trailing update is paired).  Row
-    // r0 + c of a previous panel is lane c's own row (slot 0), so its D-scaled
-    // entries are broadcast with v_readlane instead of a serialised LDS broadcast load
-    for (int q = 0; jp >= 0 && q < nprev; ++q) {
-        double li[RS][CB], ld[CB];
-#pragma unroll
-        for (int t = 0; t < RS; ++t)
-#pragma unroll
-            for (int c = 0; c < CB; c += 2) {
-                const double2v v = ld2(H + ro[t] + jp + q * CB + c);
-                li[t][c] = v.x;
-                li[t][c + 1] = v.y;
-            }
-#pragma unroll
-        for (int c = 0; c < CB; ++c) ld[c] = li[0][c] * dprev[q * CB + c];
-#pragma unroll
-        for (int c = 0; c < CB; ++c) {
-            double lk[CB];
-#pragma unroll
-            for (int c2 = 0; c2 < CB; ++c2) lk[c2] = readlane_d(ld[c2], c);
-#pragma unroll
-            for (int t = 0; t < RS; ++t) {
-                double sacc = 0.0;
-#pragma unroll
-                for (int c2 = 0; c2 < CB; c2 += 2) sacc += li[t][c2] * lk[c2] + li[t][c2 + 1] * lk[c2 + 1];
-                p[t][c] -= sacc;
-            }
-        }
-    }
-#pragma unroll
-    for (int t = 0; t < RS; ++t) {
-        const int i = r0 + lane + 64 * t;
-#pragma unroll
-        for (int c = 0; c < CB; ++c)
-            p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
-    }
-    PROF_ACC_FINE(19);
-    int bad = 0;
-#pragma unroll
-    for (int c = 0; c < CB; ++c) {
-        const double D = readlane_d(p[0][c], c);
-        bad |= !(D > 0.0) || !isfinite(D);
-        const double inv = recip(D);
-#pragma unroll
-        for (int c2 = c + 1; c2 < CB; ++c2) {
-            const double lc = readlane_d(p[0][c], c2) * inv;
-#pragma unroll
-            for (int t = 0; t < RS; ++t) p[t][c2] -= p[t][c] * lc;
-        }
-#pragma unroll
-        for (int t = 0; t < RS; ++t) p[t][c] *= inv;
-        if (lane == 0 && c < jb) {
-            dinv[r0 + c] = inv;
-            dout[c] = D;
-        }
-    }
-    PROF_ACC_FINE(20);
-    // 16-byte pair stores: the pair (c, c + 1) of row i is inside the row or its
-    // even-length padding whenever r0 + c <= i (r0 and c even), and column n of the
-    // last row is the spare row the plan allocates
-#pragma unroll
-    for (int t = 0; t < RS; ++t) {
-        const int i = r0 + lane + 64 * t;
-        if (i < n) {
-#pragma unroll
-            for (int c = 0; c < CB; c += 2)
-                if (c < jb && c <= lane + 64 * t) st2(H + ro[t] + r0 + c, double2v{p[t][c], p[t][c + 1]});
-        }
-    }
-    if (lane == 0) flag[0] = bad;
-    PROF_ACC_FINE(21);
-}
-
 // Rank-CB update of panel j0 (pivots dcur) on rows/columns >= r1, by threads
 // [t0, t0 + nth) of the workgroup.  2x2 tiles (ti >= tk) enumerated linearly
 // so every thread gets ceil(ntile / nth) tiles; two tiles per pass so their
@@ -1523,9 +1386,6 @@ __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, con
 // the diagonal of a diagonal tile and outside the matrix are neither read nor
 // written (packed rows end at the diagonal).
 typedef double double4v __attribute__((ext_vector_type(4)));
-#ifndef SCPQP_MFMA_TRAIL
-#define SCPQP_MFMA_TRAIL 1
-#endif
 
 // U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
 // budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
@@ -1603,22 +1463,16 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
 // others; the lead's look-ahead covers every panel factored since the last group
 // update.  1/G of the passes over the factor, at the price of G - 1 exposed panel
 // chains per group (G = 2: c3 3.51-3.55k -> 4.04-4.07k solves/s).
-#ifndef SCPQP_GROUP
-#define SCPQP_GROUP 2
-#endif
-static_assert(SCPQP_GROUP == 1 || SCPQP_GROUP == 2 || SCPQP_GROUP == 4, "group of 1, 2 or 4 panels");
-static_assert(2 * SCPQP_GROUP * CB <= 64, "the pivot buffer holds 64 entries");
-#ifndef SCPQP_SPLIT
-#define SCPQP_SPLIT 1
-#endif
+constexpr int kGroup = 2;   // panels per grouped trailing update (4 measured slower)
+static_assert(2 * kGroup * CB <= 64, "the pivot buffer holds 64 entries");
 
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int n = __builtin_amdgcn_readfirstlane(L.n);
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
-    constexpr int G = (LT::HGLOBAL && SCPQP_MFMA_TRAIL) ? SCPQP_GROUP : 1;
+    constexpr int G = LT::HGLOBAL ? kGroup : 1;
     lint* flag = (lint*)(L.red + 120);   // [step parity]
-    ldouble* ldbuf = L.red;              // [CB][CB] look-ahead rows (panel_factor2; red is idle here)
+    ldouble* ldbuf = L.red;              // [CB][CB] look-ahead rows (panel_factor; red is idle here)
     ldouble* dbuf = L.red + 128;         // pivots [step mod 2G][CB]; a group's slots are adjacent
     PROF_T0();
     for (int r0 = 0, s = 0; r0 < n; r0 += CB, ++s) {
@@ -1632,9 +1486,6 @@ __device__ bool cholesky(const LT& L) {
         // jp < 0 and the pointer is not dereferenced
         const ldouble* dprev = dbuf + ((s - np) & (2 * G - 1)) * CB;
         if (is_lead(L.lead)) {
-#ifdef SCPQP_PROBE_NOPANEL   // tools/probe/chol_probe.hip: time without the panel chain
-            if ((threadIdx.x & 63) == 0) flag[par] = 0;
-#else
             // rows r0 .. n-1 only: once they fit one slot per lane the panel
             // runs with one register row (half the VALU work of the chain)
             ldouble* dn = dbuf + (s % (2 * G)) * CB;
@@ -1642,19 +1493,11 @@ __device__ bool cholesky(const LT& L) {
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             lead_prio_down();
-#endif
-        } else if ((jp >= 0 || (SCPQP_SPLIT && s >= 3)) && r0 < n
-#ifdef SCPQP_PROBE_NOTRAIL   // tools/probe/chol_probe.hip: time without the trailing update
-                   && r0 < 0
-#endif
-                   ) {
+        } else if ((jp >= 0 || (G == 2 && s >= 3)) && r0 < n) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
-            if constexpr (LT::HGLOBAL && SCPQP_MFMA_TRAIL) {
-#ifndef SCPQP_TRAIL_U2
-#define SCPQP_TRAIL_U2 4
-#endif
-                constexpr int U = LT::OCCV >= 3 ? 2 : SCPQP_TRAIL_U2;   // tiles in flight per wave
-                if constexpr (G == 2 && SCPQP_SPLIT) {
+            if constexpr (LT::HGLOBAL) {
+                constexpr int U = LT::OCCV >= 3 ? 2 : 4;   // tiles in flight per wave
+                if constexpr (G == 2) {
                     // the pair's update in two halves: the left tile columns (they hold
                     // the next two panels) on the even step, the rest on the odd step,
                     // so the odd step's panel chain runs beside the trailing update
@@ -1697,13 +1540,8 @@ __device__ bool cholesky(const LT& L) {
 // are faster in isolation but slower inside the kernel, the third is slower.)
 // ---------------------------------------------------------------------------
 
-#ifndef SCPQP_SCH
-#define SCPQP_SCH 4     // chunk of a factor in LDS
-#endif
-
-#ifndef SCPQP_SCH_G
-#define SCPQP_SCH_G 8   // chunk of a factor in the workspace: twice the steps cover the L2 latency
-#endif
+constexpr int kSolveChunk = 4;    // chunk of a factor in LDS
+constexpr int kSolveChunkG = 8;   // chunk of a factor in the workspace: twice the steps cover the L2 latency
 template <int R, class HP, int SCH>
 struct Solver {   // SCH: chunk (columns / rows) streamed per step group
     static_assert(SCH % 2 == 0 && 64 % SCH == 0, "chunks tile the 64-row slots");
@@ -1825,7 +1663,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
 
 template <int R, class LT>
 __device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, ldouble* x) {
-    Solver<R, decltype(L.H), (LT::HGLOBAL ? SCPQP_SCH_G : SCPQP_SCH)> S(L.H, L.dinv, L.n, L.ld, bvec);
+    Solver<R, decltype(L.H), (LT::HGLOBAL ? kSolveChunkG : kSolveChunk)> S(L.H, L.dinv, L.n, L.ld, bvec);
     S.run(x);
 }
 
@@ -2069,10 +1907,7 @@ struct D4 {
 // x stops moving (|dx| <= tol max(1, |x|)), 2 when the iterate shows the active
 // set is wrong (warm rounds: a violated inactive row or a negative active
 // multiplier beyond `early`), 0 to continue.  Never before the second solve.
-#ifndef SCPQP_POLISH_TOL
-#define SCPQP_POLISH_TOL 1e-9
-#endif
-constexpr double kPolishTol = SCPQP_POLISH_TOL;
+constexpr double kPolishTol = 1e-9;
 // The polish penalty (warm and cold rounds alike) is polish_delta; 1/delta of the
 // current round lives in red[kIdlSlot] (set by the prep phases).  A separate warm
 // penalty was measured and not kept.
@@ -2163,10 +1998,6 @@ PHASE void ph_init_a(Ctx c) {
     for (int e = tid; e < L.n; e += NT) L.dz[e] = 0.0;
     __syncthreads();
 }
-#ifndef SCPQP_INIT_OMEGA
-#define SCPQP_INIT_OMEGA 1
-#endif
-#if SCPQP_INIT_OMEGA
 // Initial point (round 3).  The CVXOPT point below starts the slack omega from the
 // normal system, where its weight (1e5, SCP_controller.py:138) drives it to -1e4 and
 // the multipliers to 1e5 spread over every row; the iterates then crawl for 5-8
@@ -2180,16 +2011,8 @@ PHASE void ph_init_a(Ctx c) {
 //    carries the slack weight at any point with omega = 0).
 // CPU study, cold IPM iterations per QP (tools/ipm_corrector_study.py): c2 15.7 -> 12.5,
 // 4 veh Hp 10 14.3 -> 10.1, Hp 30 16.0 -> 13.0, parallel5 23.1 -> 18.0, frog 16.7 -> 14.7;
-// every QP's polish certifies the same minimiser.
-// A/B variant (SCPQP_INIT_ZERO): start the controls at 0 and skip the initial solve
-#ifndef SCPQP_INIT_ZERO
-#define SCPQP_INIT_ZERO 0
-#endif
-PHASE void ph_init_zero(Ctx c) {
-    LAYDEF;
-    for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] = 0.0;
-    __syncthreads();
-}
+// every QP's polish certifies the same minimiser.  (CVXOPT's own point, and starting the
+// controls at 0 without the initial solve, were measured and not kept: DESIGN §3.)
 PHASE void ph_init_decouple(Ctx c) {
     LAYDEF;
     const int N = L.N, o = roff(N);
@@ -2230,33 +2053,6 @@ PHASE void ph_init_b(Ctx c) {
     if (tid == 0) L.z[N] = om;
     __syncthreads();
 }
-#else
-// s = h - G z, lam = -s, CVXOPT positivity shifts
-PHASE void ph_init_b(Ctx c) {
-    LAYDEF;
-    const int tid = threadIdx.x;
-    g_apply(L, L.z, L.s, false);
-    double smin = 1e300, ssq = 0.0, smax = -1e300;
-    for (int r = tid; r < L.mc; r += NT) {
-        const double sv = hval(L, r) - L.s[r];
-        L.s[r] = sv;
-        L.lam[r] = -sv;
-        smin = fmin(smin, sv);
-        smax = fmax(smax, sv);
-        ssq += sv * sv;
-    }
-    double red[4] = {-smin, ssq, smax, 0.0};
-    block_reduce4<3>(red, 5, L.red);
-    const double ts = red[0], nrm = sqrt(red[1]), tz = red[2];   // tz = -min(lam) = max(s)
-    const bool shs = ts >= -1e-8 * fmax(nrm, 1.0);
-    const bool shz = tz >= -1e-8 * fmax(nrm, 1.0);
-    for (int r = tid; r < L.mc; r += NT) {
-        if (shs) L.s[r] += 1.0 + ts;
-        if (shz) L.lam[r] += 1.0 + tz;
-    }
-    __syncthreads();
-}
-#endif
 // Interior-point step bodies.  The phase functions below chain several of
 // them in one out-of-line call: every call costs its register save/restore
 // and layout rebuild (~2k cycles for a trivial phase), and the bodies of one
@@ -2309,12 +2105,8 @@ __device__ __forceinline__ double affine_body(const LT& L, double mu) {
 // iteration's residuals absorb.  CPU study, cold IPM iterations per QP: c2 11.4 -> 10.9,
 // Hp 30 11.0 -> 10.1, c3 14.0 -> 13.1 (max 23 -> 19), frog 15.9 -> 11.0; Hp 10 and
 // parallel5 unchanged; every polish certifies the same minimiser.
-#ifndef SCPQP_SPLIT_STEP
-#define SCPQP_SPLIT_STEP 1
-#endif
 template <class LT>
 __device__ __forceinline__ void update_body(const LT& L, double eta) {
-#if SCPQP_SPLIT_STEP
     // separate step lengths: (z, s) by the primal ratio test, lam by the dual one
     double ap = 1.0, ad = 1.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
@@ -2330,29 +2122,18 @@ __device__ __forceinline__ void update_body(const LT& L, double eta) {
         L.s[r] += ap * L.ds[r];
         L.lam[r] += ad * L.dl[r];
     }
-#else
-    const double alpha = fmin(1.0, eta * max_step(L));
-    for (int e = threadIdx.x; e < L.n; e += NT) L.z[e] += alpha * L.dz[e];
-    for (int r = threadIdx.x; r < L.mc; r += NT) {
-        L.s[r] += alpha * L.ds[r];
-        L.lam[r] += alpha * L.dl[r];
-    }
-#endif
     __syncthreads();
 }
 // Fraction of the step to the boundary (round 3): max(0.99, 1 - mu) instead of a fixed
 // 0.99, i.e. nearly full steps once the scaled complementarity is small.  CPU study
 // (tools/ipm_corrector_study.py, from the round-3 start): cold IPM iterations per QP
 // c2 12.5 -> 11.5, 4 veh Hp 10 10.1 -> 7.8, parallel5 18.0 -> 16.6, frog 14.7 -> 12.0.
-#ifndef SCPQP_STEP_ADAPTIVE
-#define SCPQP_STEP_ADAPTIVE 1
-#endif
-__device__ __forceinline__ double step_factor(double mu) {
-    return SCPQP_STEP_ADAPTIVE ? fmax(0.99, 1.0 - mu) : 0.99;
-}
-// d = lam / s, K = P + G' diag(d) G, and the predictor right-hand side (rc = s lam;
-// it does not need the factor, so it is formed before the factorisation)
-PHASE void ph_scale_assemble_rhs(Ctx c) {
+__device__ __forceinline__ double step_factor(double mu) { return fmax(0.99, 1.0 - mu); }
+// d = lam / s, K = P + G' diag(d) G, the predictor right-hand side (rc = s lam; it does
+// not need the factor, so it is formed before the factorisation) and L D L' of K in one
+// call (one call fewer per IPM iteration than assembly and factorisation apart: c2 +0.8 %,
+// profiles/r03_ab_fuse_fact.txt).  1 = factored.
+PHASE int ph_scale_assemble_rhs_factor(Ctx c) {
     LAYDEF;
     PROF_T0_FINE();
     for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
@@ -2362,17 +2143,6 @@ PHASE void ph_scale_assemble_rhs(Ctx c) {
     PROF_ACC_FINE0(29);
     newton_rhs_body(L, 0, 0.0);
     PROF_ACC_FINE0(28);
-}
-// the same, then L D L' of K in the same call (SCPQP_FUSE_FACT); 1 = factored
-#ifndef SCPQP_FUSE_FACT
-#define SCPQP_FUSE_FACT 1
-#endif
-PHASE int ph_scale_assemble_rhs_factor(Ctx c) {
-    LAYDEF;
-    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
-    __syncthreads();
-    assemble(P, L, L.dd, 0.0);
-    newton_rhs_body(L, 0, 0.0);
     return cholesky(L) ? 1 : 0;
 }
 // polish: K = P + rho I + G_A' G_A / delta, factored in the same call
@@ -2393,31 +2163,6 @@ PHASE double ph_back_affine_rhs(Ctx c, double mu) {
 // point (the next iteration's convergence test)
 PHASE D4 ph_back_update_residuals(Ctx c, double smu, double eta) {
     LAYDEF;
-    newton_back_body(L, 1, smu);
-    update_body(L, eta);
-    double r[4];
-    residuals(P, L, r);
-    return D4{r[0], r[1], r[2], r[3]};
-}
-// Fused solve phases (round 3, SCPQP_FUSE_SOLVE): the triangular solve and the vector
-// phase after it in one out-of-line call.  A call costs its callee-saved register
-// spills and restores through the private stack (280 B per lane, the source of c2's
-// write traffic) and the layout rebuild; the two bodies run one after the other, so
-// the fused function's register budget is the larger of the two, not their sum.
-#ifndef SCPQP_FUSE_SOLVE
-#define SCPQP_FUSE_SOLVE 0
-#endif
-PHASE double ph_solve_back_affine_rhs(Ctx c, double mu) {
-    LAYDEF;
-    chol_solve(L, L.rhs, L.dz);
-    newton_back_body(L, 0, 0.0);
-    const double smu = affine_body(L, mu);
-    newton_rhs_body(L, 1, smu);
-    return smu;
-}
-PHASE D4 ph_solve_back_update_residuals(Ctx c, double smu, double eta) {
-    LAYDEF;
-    chol_solve(L, L.rhs, L.dz);
     newton_back_body(L, 1, smu);
     update_body(L, eta);
     double r[4];
@@ -2508,13 +2253,6 @@ PHASE D4 ph_polish_dual_next(Ctx c, int ref, int cap, double early) {
     if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
     return d;
 }
-PHASE D4 ph_solve_polish_dual_next(Ctx c, int ref, int cap, double early) {
-    LAYDEF;
-    chol_solve(L, L.rhs, L.dz);
-    const D4 d = polish_dual_body(P, L);
-    if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
-    return d;
-}
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
 // Otherwise one primal-dual active-set correction (oracle _pdas_update): add the
 // violated inactive rows, drop the active rows with negative multipliers, and
@@ -2601,17 +2339,8 @@ PHASE void ph_trace_sol(Ctx c, double* dst, D4 ev, double delta, int ipm, int qf
 // Active-set corrections of the polish (oracle POLISH_ROUNDS), the rounds a
 // warm start may take before the IPM runs, and the multiplier iteration's
 // convergence test (oracle POLISH_TOL).
-#ifndef SCPQP_POLISH_ROUNDS
-#define SCPQP_POLISH_ROUNDS 6
-#endif
-#ifndef SCPQP_POLISH_EXTEND
-#define SCPQP_POLISH_EXTEND 1
-#endif
-constexpr int kPolishRounds = SCPQP_POLISH_ROUNDS;
-#ifndef SCPQP_WARM_ROUNDS
-#define SCPQP_WARM_ROUNDS 8
-#endif
-constexpr int kWarmRounds = SCPQP_WARM_ROUNDS;
+constexpr int kPolishRounds = 6;
+constexpr int kWarmRounds = 8;        // 4 measured within noise or slower
 constexpr int kWarmRefine = 12;       // solve cap per warm round (cold rounds: P.nRefine)
 // Warm rounds stop refining as soon as the iterate shows the active set is
 // wrong (an inactive row violated, or an active multiplier negative, by more
@@ -2625,10 +2354,7 @@ constexpr double kWarmEarly = 1e-6;
 // of c2-size problems still certified often enough that the rule cost c2 1-2 %
 // (tools/warm_policy_study.py); with the 1e-9 tolerance it gains c2 2-3 %
 // (profiles/r02_ab_warm_stall.txt), so it applies to every plan.
-#ifndef SCPQP_WARM_STALL
-#define SCPQP_WARM_STALL 1
-#endif
-constexpr bool kWarmStall = SCPQP_WARM_STALL;
+constexpr bool kWarmStall = true;
 
 // ---------------------------------------------------------------------------
 // QP driver: Mehrotra predictor-corrector IPM + active-set polish (scaled
@@ -2653,24 +2379,15 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, in
     for (int round = 0; round < max_rounds && !ok; ++round) {
         ++st.rounds;
         if (refactor) {
-#if SCPQP_FUSE_FACT
             const bool fact = PH(ph_assemble_factor)(c, rho) != 0;
-#else
-            PH(ph_assemble)(c, rho);
-            const bool fact = PH(ph_cholesky)(c) != 0;
-#endif
             PROF_ACC(7);
             if (!fact) break;
         }
         int conv = 0;
         PH(ph_polish_rhs)(c);
         for (int ref = 0; ref < cap; ++ref) {
-#if SCPQP_FUSE_SOLVE
-            const D4 d = PH(ph_solve_polish_dual_next)(c, ref, cap, early);
-#else
             PH(ph_solve)(c, 1);
             const D4 d = PH(ph_polish_dual_next)(c, ref, cap, early);
-#endif
             ++st.refine;
             const int stop = polish_stop(d, ref, early);
             conv = stop == 1;
@@ -2682,7 +2399,7 @@ __device__ __forceinline__ bool polish_rounds(Ctx c, double hmax, double rho, in
         // acc >= 2: active set corrected -> refactor;  acc 0 with the multiplier
         // iteration still moving: same active set, keep iterating on the same
         // factor;  acc 0 after convergence: stuck, give up
-        if (acc == 0 && (conv || extended || !SCPQP_POLISH_EXTEND)) break;
+        if (acc == 0 && (conv || extended)) break;
         if (acc >= 2) {
             if (stall && round >= 1 && acc - 1 >= prev_chg) break;
             prev_chg = acc - 1;
@@ -2721,18 +2438,12 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     // ---- initial point: (P + G'G) x = -q + G'h (omega decoupled, see ph_init_b);
     // s = h - Gx and lam from ph_init_b
     PROF_T0();
-#if SCPQP_INIT_ZERO
-    PH(ph_init_zero)(c);
-#else
     PH(ph_init_a)(c);
     PH(ph_assemble)(c, 0.0);
-#if SCPQP_INIT_OMEGA
     PH(ph_init_decouple)(c);
-#endif
     PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
     PH(ph_rhs_from_tv)(c, 0.0);
     PH(ph_solve)(c, 0);
-#endif
     PH(ph_init_b)(c);
     PROF_ACC(16);
     // ---- Mehrotra iterations
@@ -2749,21 +2460,8 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
                 break;
             }
             const double mu = res.c / mc;
-#if SCPQP_FUSE_FACT
             if (!PH(ph_scale_assemble_rhs_factor)(c)) break;
             PROF_ACC(3);
-#else
-            PH(ph_scale_assemble_rhs)(c);
-            PROF_ACC(2);
-            if (!PH(ph_cholesky)(c)) break;
-            PROF_ACC(3);
-#endif
-#if SCPQP_FUSE_SOLVE
-            const double smu = PH(ph_solve_back_affine_rhs)(c, mu);
-            PROF_ACC(5);
-            res = PH(ph_solve_back_update_residuals)(c, smu, step_factor(mu));
-            PROF_ACC(6);
-#else
             PH(ph_solve)(c, 1);
             PROF_ACC(9);
             const double smu = PH(ph_back_affine_rhs)(c, mu);
@@ -2772,7 +2470,6 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
             PROF_ACC(9);
             res = PH(ph_back_update_residuals)(c, smu, step_factor(mu));
             PROF_ACC(6);
-#endif
         }
         // the iteration cap counts against the QP only in the first pass: a resumed pass
         // (below) runs 100x tighter than the QP's tolerance, which it has already met
@@ -3056,7 +2753,7 @@ __global__ __launch_bounds__(kOrderThreads) void order_kernel(const int* hp, int
 // ---------------------------------------------------------------------------
 // Host side (left out of device-only probe builds: tools/probe/)
 // ---------------------------------------------------------------------------
-#ifdef SCPQP_NO_HOST
+#ifdef SCPQP_DIAG_NO_HOST
 }  // namespace
 #else
 thread_local char g_err[512] = "";
@@ -3107,7 +2804,11 @@ int plan(scpqp_handle* h) {
     // ~2.7x slower (4 vehicles at Hp 30: profiles/r03_c5_classes.txt); among the rest,
     // the most workgroups per CU (the kernel is latency-bound), then less in global
     // memory.
-    const char* force = getenv("SCPQP_PLAN");   // diagnostic: force a plan
+#ifdef SCPQP_DIAG
+    const char* force = getenv("SCPQP_PLAN");   // diagnostic build: force a plan
+#else
+    const char* force = nullptr;
+#endif
     const int cfg0 = force ? atoi(force) : 0, cfg1 = force ? cfg0 + 1 : 3;
     int best = -1, bestPer = 0, bestKey = -1;
     bool bestLean = false;
@@ -3157,10 +2858,12 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     if (a.B <= 0) return 0;
     HIPCHK(hipSetDevice(h->device));
     int grid = a.B < h->grid ? a.B : h->grid;
-    if (const char* g = getenv("SCPQP_GRID")) {   // diagnostic: fewer resident workgroups
+#ifdef SCPQP_DIAG
+    if (const char* g = getenv("SCPQP_GRID")) {   // diagnostic build: fewer resident workgroups
         const int cap = atoi(g);
         if (cap > 0 && cap < grid) grid = cap;
     }
+#endif
     if (h->wsStride > 0) {
         const size_t need = (size_t)grid * h->wsStride * sizeof(double);
         if (need > h->wsBytes) {
@@ -3176,8 +2879,13 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     a.counter = h->counter;
     HIPCHK(hipMemsetAsync(h->counter, 0, sizeof(int), st));
     a.perm = nullptr;
-    const char* ord = getenv("SCPQP_ORDER");   // diagnostic: SCPQP_ORDER=0 keeps the input order
-    if (a.mode == MODE_SOLVE && a.hp && h->perm && !(ord && atoi(ord) == 0)) {
+#ifdef SCPQP_DIAG
+    const char* ord = getenv("SCPQP_ORDER");   // diagnostic build: SCPQP_ORDER=0 keeps the input order
+    const bool keep_order = ord && atoi(ord) == 0;
+#else
+    const bool keep_order = false;
+#endif
+    if (a.mode == MODE_SOLVE && a.hp && h->perm && !keep_order) {
         hipLaunchKernelGGL(order_kernel, dim3(1), dim3(kOrderThreads), 0, st, a.hp, a.B, h->dims.hp_max,
                            h->perm);
         HIPCHK(hipGetLastError());
@@ -3190,12 +2898,14 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
     int sh = 0;
     if (d.n_obst == 0 && d.n_veh == 4) sh = (d.hp_max == 20 && !a.hp) ? 1 : 2;
     if (d.n_obst == 0 && d.n_veh == 8 && d.hp_max == 30 && !a.hp) sh = 3;
-    if (const char* e = getenv("SCPQP_SHAPE"))   // diagnostic: SCPQP_SHAPE=0 runs the runtime shape
+#ifdef SCPQP_DIAG
+    if (const char* e = getenv("SCPQP_SHAPE"))   // diagnostic build: SCPQP_SHAPE=0 runs the runtime shape
         if (atoi(e) == 0) sh = 0;
-#ifdef SCPQP_ONLY_C2
+#endif
+#ifdef SCPQP_DIAG_C2ONLY
     // diagnostic build (fast compile for A/B work): the c2 / c4 instantiations only
     if (R != 2 || occ != 3 || h->hG || !h->vG)
-        return fail(SCPQP_E_SIZE, "SCPQP_ONLY_C2 build: c2-shaped problems only%s");
+        return fail(SCPQP_E_SIZE, "SCPQP_DIAG_C2ONLY build: c2-shaped problems only%s");
     if (sh == 1) return launch_t<false, true, 2, 3, 1>(h, a, st, grid);
     return launch_t<false, true, 2, 3, 0>(h, a, st, grid);
 #else
@@ -3455,4 +3165,4 @@ int scpqp_resources(scpqp_handle* h, int64_t* lds, int64_t* ws, int32_t* big, in
 }
 
 }  // extern "C"
-#endif  // SCPQP_NO_HOST
+#endif  // SCPQP_DIAG_NO_HOST

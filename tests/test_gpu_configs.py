@@ -137,28 +137,91 @@ def test_c5_mixed_horizon_full_batch_3072(gpu):
     S.close()
 
 
-def test_c3_capped_problems_at_full_tolerance(gpu):
-    """c3 problems that hit the reference's 20-QP cap (the SCP loop ends at max_scp without
-    meeting its stopping rule, SCP_controller.py:40-49, 191-195; ~12 % of c3) are held to
-    the same tolerances as converged ones, not exempted.  Problems 14 and 18 of the seed-0
-    stream run 20 SCP iterations in the restatement; for these two the restatement's own exact
-    and regularised polish modes agree to 2e-10 m over all 20 iterations, so 1e-6 m / 1e-7 rad
-    apply.  (Other capped c3 problems are path-sensitive: changing the IPM tolerance moves
-    their last iterate by up to 1.2e-5 rad, profiles/r03_ab_ipm_tol_final.txt.)"""
-    sc = R.circle_scenario(8, Hp=30)
-    B = 24
-    bt = shard.shard_batch(sc, B, 0, base_seed=0)
-    S = ScpQpSolver(sc, max_batch=B)
-    out = S.solve(bt.x0, bt.u0, bt.ec_noise, trace=True)
-    torch.cuda.synchronize()
-    idx = [14, 18]
-    jobs = [(8, 30, bt.x0[b], bt.u0[b], bt.ec_noise[b]) for b in idx]
-    with mp.get_context("spawn").Pool(2) as pool:
-        res = pool.map(_oracle_job, jobs)
-    for b, r in zip(idx, res):
-        assert r.n_scp == R.MAX_SCP_ITER and not r.converged
-        ub, tb = unpack_problem(out, b, 8, 30)
-        c = SP.compare(ub.cpu().numpy(), tb.cpu().numpy(), int(out.n_scp[b].item()),
-                       SP.device_trace(out, b, 8, 0, 30, 30), r, 8, 30, what=f"c3 capped problem {b}")
-        assert int(out.n_scp[b].item()) == R.MAX_SCP_ITER and not c["mismatch"]
-    S.close()
+def _oracle_modes_job(args):
+    """Both polish modes of the restatement on one problem (exact KKT polish and the
+    device's regularised one): the restatement's own mode-to-mode spread."""
+    r_exact = _oracle_job(args)
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (here, root, os.path.join(root, "senquential-convex-programming-for-trajectory-planning_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import scp_reference as R_
+    n_veh, hp, x0, u0, ec = args[:5]
+    sc = R_.circle_scenario(n_veh, Hp=hp)
+    p = R_.make_problem(sc, x0, u0, ec, Hp=hp)
+    r_reg = R_.scp_solve(p, mode="structured", keep_history=True, polish="regularised")
+    return r_exact, r_reg
+
+
+# Capped problems (the SCP loop ends at the reference's 20-QP cap without meeting its
+# stopping rule, SCP_controller.py:86, 191-195).  Their iterates oscillate, so rounding
+# differences that the stopping rule forgives on a converged problem are carried through
+# all 20 iterations.  Every capped problem is compared per SCP iteration against the
+# restatement (exact-polish mode).  The tolerance, per iteration it:
+#     |u_dev(it) - u_exact(it)| <= max(CAPPED_U_TOL, U_TOL + |u_reg(it) - u_exact(it)|)
+# i.e. the converged-problem tolerance (1e-7 rad) widened by the restatement's own spread
+# between its two polish modes at that iteration (the reference's answer is not pinned
+# more tightly than that: both modes certify a KKT point of the same QP), with a floor
+# CAPPED_U_TOL = 1e-5 rad, the spread of the device's own capped c3 iterates between two
+# IPM tolerances (1e-9 vs 3e-9, DESIGN §3: up to 1.2e-5 rad).  The final u and trajectory
+# are held to CAPPED_U_TOL and CAPPED_TRAJ_TOL = 1e-4 m.
+CAPPED_U_TOL = 1e-5
+CAPPED_TRAJ_TOL = 1e-4
+
+
+def _check_capped(out, b, nV, H, r_exact, r_reg, what):
+    assert r_exact.n_scp == R.MAX_SCP_ITER and not r_exact.converged, what
+    assert int(out.n_scp[b].item()) == R.MAX_SCP_ITER, what
+    tr = SP.device_trace(out, b, nV, 0, H, H)
+    N = nV * H
+    e_dev = e_mode = 0.0
+    for it in range(R.MAX_SCP_ITER):
+        ed = float(np.max(np.abs(tr[it]["z"][:N] - r_exact.history[it]["z"][:N])))
+        em = (float(np.max(np.abs(r_reg.history[it]["z"][:N] - r_exact.history[it]["z"][:N])))
+              if it < r_reg.n_scp else 0.0)
+        assert ed <= max(CAPPED_U_TOL, SP.U_TOL + em), \
+            f"{what}: iteration {it} |u| err {ed:.2e} rad, restatement mode spread {em:.2e}"
+        e_dev, e_mode = max(e_dev, ed), max(e_mode, em)
+    ub, tb = unpack_problem(out, b, nV, H)
+    e_u = float(np.max(np.abs(ub.cpu().numpy() - r_exact.u)))
+    e_t = float(np.max(np.abs(tb.cpu().numpy() - r_exact.traj)))
+    print(f"{what}: per-iteration |u| err {e_dev:.2e} rad, final |u| {e_u:.2e} rad, "
+          f"|traj| {e_t:.2e} m; restatement mode spread {e_mode:.2e} rad")
+    assert e_u <= CAPPED_U_TOL, what
+    assert e_t <= CAPPED_TRAJ_TOL, what
+    return e_dev, e_mode
+
+
+def test_capped_problems_within_stated_tolerance(gpu):
+    """Every capped problem of the c2 batch (B = 1024) and of the first 32 problems of the
+    c3 stream, per SCP iteration against the restatement, to CAPPED_U_TOL (above).
+    Problems 14 and 18 of the c3 stream, whose two restatement modes agree to 2e-10 m over
+    all 20 iterations, are held to the converged-problem tolerances (1e-7 rad)."""
+    worst = {}
+    for nV, Hp, B in ((4, 20, 1024), (8, 30, 32)):
+        sc = R.circle_scenario(nV, Hp=Hp)
+        bt = shard.shard_batch(sc, B, 0, base_seed=0)
+        S = ScpQpSolver(sc, max_batch=B)
+        out = S.solve(bt.x0, bt.u0, bt.ec_noise, trace=True)
+        torch.cuda.synchronize()
+        st = out.status.cpu().numpy()
+        capped = np.flatnonzero((st & 0xff) == LB.ST_MAX_SCP).tolist()
+        assert capped, f"no capped problem in the {nV}-vehicle sample"
+        jobs = [(nV, Hp, bt.x0[b], bt.u0[b], bt.ec_noise[b]) for b in capped]
+        with mp.get_context("spawn").Pool(min(16, len(jobs))) as pool:
+            res = pool.map(_oracle_modes_job, jobs)
+        for b, (r_exact, r_reg) in zip(capped, res):
+            e_dev, e_mode = _check_capped(out, b, nV, Hp, r_exact, r_reg, f"{nV} veh capped problem {b}")
+            worst[(nV, b)] = (e_dev, e_mode)
+            if nV == 8 and b in (14, 18):
+                c = SP.compare(*[t.cpu().numpy() for t in unpack_problem(out, b, 8, 30)],
+                               int(out.n_scp[b].item()), SP.device_trace(out, b, 8, 0, 30, 30), r_exact,
+                               8, 30, what=f"c3 capped problem {b} at the converged tolerances")
+                assert not c["mismatch"]
+        S.close()
+    print("capped problems compared:", len(worst), "worst device error",
+          f"{max(v[0] for v in worst.values()):.2e}", "worst mode spread",
+          f"{max(v[1] for v in worst.values()):.2e}")

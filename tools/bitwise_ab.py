@@ -1,0 +1,68 @@
+"""Bitwise A/B of two builds of the library on one configuration: solve the same batch
+with each (one process per library, SCPQP_LIB) and compare every output array exactly.
+
+    python tools/bitwise_ab.py <config c2|c4|c5|c3> <lib_a.so> <lib_b.so> [batch]
+"""
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd")]
+
+CFG = {"c2": (4, 20, 1024, None), "c4": (4, 20, 8192, None), "c3": (8, 30, 4096, None),
+       "c5": (4, 30, 3072, (10, 20, 30))}
+
+
+def run_one(cfg, out_path, batch):
+    import torch
+    import Scenarios
+    from scpqp import shard
+    from scpqp.solver import ScpQpSolver
+    nv, hp, B, mixed = CFG[cfg]
+    B = batch or B
+    sc = Scenarios.Scenario(False)
+    sc.Hp = sc.Hu = hp
+    sc.get_circle_scenario([2 * np.pi / nv * (i + 1) for i in range(nv)])
+    sc.complete_scenario()
+    bt = shard.shard_batch(sc, B, 0, base_seed=0, mixed_hp=mixed)
+    S = ScpQpSolver(sc, max_batch=B)
+    out = S.solve(bt.x0, bt.u0, bt.ec_noise, hp=bt.hp if mixed else None)
+    torch.cuda.synchronize()
+    np.savez(out_path, **{k: getattr(out, k).cpu().numpy() for k in
+                          ("u", "traj", "status", "n_scp", "n_ipm", "obj", "max_violation",
+                           "n_polish", "n_refine", "n_warm")})
+    S.close()
+
+
+def main():
+    if sys.argv[1] == "--one":
+        run_one(sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 0)
+        return
+    cfg, la, lb = sys.argv[1:4]
+    batch = sys.argv[4] if len(sys.argv) > 4 else "0"
+    res = []
+    for lib in (la, lb):
+        fd, path = tempfile.mkstemp(suffix=".npz")
+        os.close(fd)
+        env = dict(os.environ, SCPQP_LIB=os.path.abspath(lib))
+        subprocess.run([sys.executable, __file__, "--one", cfg, path, batch], env=env, check=True)
+        res.append(dict(np.load(path)))
+        os.unlink(path)
+    same = True
+    for k in res[0]:
+        eq = np.array_equal(res[0][k], res[1][k])
+        same &= eq
+        if not eq:
+            d = np.abs(res[0][k].astype(float) - res[1][k].astype(float))
+            print(f"{cfg} {k}: DIFFERS (max |diff| {d.max():.3e}, {int((d != 0).sum())} entries)")
+    print(f"{cfg}: {os.path.basename(la)} vs {os.path.basename(lb)}: "
+          f"{'bitwise identical' if same else 'DIFFERENT'} ({len(res[0]['n_scp'])} problems)")
+    sys.exit(0 if same else 1)
+
+
+if __name__ == "__main__":
+    main()

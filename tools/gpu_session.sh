@@ -2,9 +2,9 @@
 # One GPU box session: A/B bench of library builds (bench.py, no CPU leg, two
 # alternating repetitions), then the GPU test suite on the shipped library.
 #   gpurun -- bash tools/gpu_session.sh <tag> "<cfg:steps ...>" "<lib.so ...>" [pytest -k expr | all | none]
-# Libraries built with -DSCPQP_ONLY_C2 serve c2-shaped problems only (c2, c4).  A library
+# Libraries built with -DSCPQP_DIAG_C2ONLY serve c2-shaped problems only (c2, c4).  A library
 # entry of the form VAR=value@lib.so runs that library with the environment variable set
-# (e.g. SCPQP_SHAPE=0@senquential-.../scpqp/libscpqp.so: the runtime-shape instantiation).
+# (e.g. SCPQP_SHAPE=0@ab/lib_diag.so: the runtime-shape instantiation of a -DSCPQP_DIAG build).
 TAG=$1; CFGS=$2; LIBS=$3; K=${4:-none}
 OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 // left out).  Cycles per L D L' solve for n = 81 (c2) and n = 121 (c5's Hp 30), one
 // workgroup alone and 3 workgroups per CU.  Variants are tried by editing Solver.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/probe/solve_probe.hip -o tools/probe/solve_probe
-#define SCPQP_NO_HOST
+#define SCPQP_DIAG_NO_HOST
 #include "../../senquential-convex-programming-for-trajectory-planning_amd/csrc/scpqp.hip"
 
 namespace {
