@@ -1947,14 +1947,6 @@ __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
     (void)P
 #define PH(f) f<HG, VG, RM, OCC, SH>
 
-PHASE void ph_assemble(Ctx c, double rho) {
-    LAYDEF;
-    assemble(P, L, L.dd, rho);
-}
-PHASE int ph_cholesky(Ctx c) {
-    LAYDEF;
-    return cholesky(L) ? 1 : 0;
-}
 // x = K^{-1} rhs into z (dst = 0) or dz (dst = 1)
 PHASE void ph_solve(Ctx c, int dst) {
     LAYDEF;
@@ -2003,7 +1995,7 @@ PHASE void ph_init_a(Ctx c) {
 // the multipliers to 1e5 spread over every row; the iterates then crawl for 5-8
 // iterations with steps of 0.1-0.4 (tools/ipm_corrector_study.py).  Instead:
 //  * the controls solve the omega-free normal system (row N of P + G'G decoupled:
-//    ph_init_decouple between the assembly and the factorisation);
+//    ph_init_assemble_factor between the assembly and the factorisation);
 //  * omega = the smallest value that satisfies every collision row, plus one;
 //  * s = h - G x, shifted positive (1.5 x its most negative entry) and floored at a
 //    tenth of its largest entry;
@@ -2013,12 +2005,6 @@ PHASE void ph_init_a(Ctx c) {
 // 4 veh Hp 10 14.3 -> 10.1, Hp 30 16.0 -> 13.0, parallel5 23.1 -> 18.0, frog 16.7 -> 14.7;
 // every QP's polish certifies the same minimiser.  (CVXOPT's own point, and starting the
 // controls at 0 without the initial solve, were measured and not kept: DESIGN §3.)
-PHASE void ph_init_decouple(Ctx c) {
-    LAYDEF;
-    const int N = L.N, o = roff(N);
-    for (int e = threadIdx.x; e <= N; e += NT) L.H[o + e] = e == N ? 1.0 : 0.0;
-    __syncthreads();
-}
 PHASE void ph_init_b(Ctx c) {
     LAYDEF;
     const int tid = threadIdx.x, N = L.N, mc = L.mc;
@@ -2150,6 +2136,16 @@ PHASE int ph_assemble_factor(Ctx c, double rho) {
     LAYDEF;
     assemble(P, L, L.dd, rho);
     return cholesky(L) ? 1 : 0;
+}
+// the cold IPM's starting system P + G'G with its omega row decoupled (row N = e_N),
+// assembled and factored in one call
+PHASE void ph_init_assemble_factor(Ctx c) {
+    LAYDEF;
+    assemble(P, L, L.dd, 0.0);
+    const int N = L.N, o = roff(N);
+    for (int e = threadIdx.x; e <= N; e += NT) L.H[o + e] = e == N ? 1.0 : 0.0;
+    __syncthreads();
+    cholesky(L);   // P + G'G is positive definite (box and omega rows)
 }
 // predictor back-substitution, affine step and centring, corrector right-hand side
 PHASE double ph_back_affine_rhs(Ctx c, double mu) {
@@ -2439,9 +2435,7 @@ __device__ __forceinline__ bool qp_solve_body(Ctx c, const QpKnobs& K, int& qfla
     // s = h - Gx and lam from ph_init_b
     PROF_T0();
     PH(ph_init_a)(c);
-    PH(ph_assemble)(c, 0.0);
-    PH(ph_init_decouple)(c);
-    PH(ph_cholesky)(c);   // P + G'G is positive definite (box and omega rows)
+    PH(ph_init_assemble_factor)(c);
     PH(ph_rhs_from_tv)(c, 0.0);
     PH(ph_solve)(c, 0);
     PH(ph_init_b)(c);
