@@ -1258,6 +1258,20 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
             p[t][c] = (i < n && c < jb) ? p[t][c] : ((t == 0 && lane == c) ? 1.0 : 0.0);
     }
     PROF_ACC_FINE(19);
+    if (jb == 1) {
+        // the last panel of n = 8 k + 1 (every shape with V Hb a multiple of 8: the omega
+        // row alone): its pivot is the updated diagonal entry.  Nothing of this panel is
+        // read later but dinv (no trailing columns, no look-ahead rows, the diagonal of L
+        // is implicit), so the 8 x 8 block factorisation, the row substitution and the
+        // stores are skipped; D and 1/D are the values they would produce.
+        const double D = readlane_d(p[0][0], 0);
+        if (lane == 0) {
+            dinv[r0] = recip(D);
+            dout[0] = D;
+            flag[0] = !(D > 0.0) || !isfinite(D);
+        }
+        return;
+    }
     // the diagonal block (lanes 0 .. 7 of slot 0), lower triangle, on uniform values
     double a[CB][CB];
 #pragma unroll
