@@ -1102,6 +1102,9 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
         (void)T4;
         (void)PV;
         assemble_tiles<2>(P, L, d, rho);
+#ifdef SCPQP_DIAG_X2_ASM   // counter attribution: the tiles again (the same values stored)
+        assemble_tiles<2>(P, L, d, rho);
+#endif
     }
     PROF_ACC_FINE0(26);
     const int N = L.N;
@@ -1341,7 +1344,9 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
 // LDS latencies overlap.  r1 is even, so the (i0, i0 + 1) element of a
 // diagonal tile is row i0's padding slot, and row n (i1 == n) is the spare
 // row the plan allocates: the tile stores need no predicates.
-template <class HP>
+// NEUTRAL (diagnostic builds only, SCPQP_DIAG_X2_TRAIL): the same loads and stores with the
+// entries unchanged, so that a second pass attributes the update's LDS bank conflicts
+template <class HP, bool NEUTRAL = false>
 __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, const ldouble* dcur,
                                                 int t0, int nth) {
     double dc[CB];
@@ -1378,10 +1383,11 @@ __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, con
             if (u2 == 1 && tb == t) break;
             const int i0 = r1 + 2 * ia[u2], k0 = r1 + 2 * ka[u2];
             const int o0 = roff(i0), o1 = roff(i0 + 1);
-            H[o0 + k0] -= sm[u2][0];
-            H[o0 + k0 + 1] -= sm[u2][1];
-            H[o1 + k0] -= sm[u2][2];
-            H[o1 + k0 + 1] -= sm[u2][3];
+            const double f = NEUTRAL ? 0.0 : 1.0;
+            H[o0 + k0] -= f * sm[u2][0];
+            H[o0 + k0 + 1] -= f * sm[u2][1];
+            H[o1 + k0] -= f * sm[u2][2];
+            H[o1 + k0 + 1] -= f * sm[u2][3];
         }
     }
 }
@@ -1525,6 +1531,9 @@ __device__ bool cholesky(const LT& L) {
                 }
             } else {
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
+#ifdef SCPQP_DIAG_X2_TRAIL   // counter attribution: a result-neutral second pass
+                trailing_update<decltype(L.H), true>(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
+#endif
             }
         }
 #if defined(SCPQP_PROF) && defined(SCPQP_PROF_FINE)
@@ -1683,6 +1692,9 @@ __device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, l
 
 template <class LT>
 __device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
+#ifdef SCPQP_DIAG_X2_SOLVE   // counter attribution: the solve twice (the same x)
+    for (int rep = 0; rep < 2; ++rep)
+#endif
     if (is_lead(L.lead)) {
         const int n = L.n;
         constexpr int RM = LT::RMAX;
