@@ -78,3 +78,20 @@ def device_trace(out, b, nV, nO, H, hp_max):
     if out.trace is None:
         return None
     return TR.decode(out.trace[b].cpu().numpy(), int(out.n_scp[b].item()), nV, nO, H, hp_max)
+
+
+def oracle_job(args):
+    """One oracle SCP solve with its per-iteration history, for a spawn pool:
+    ``args`` = (n_veh, Hp, x0, u0, ec_noise[, scenario Hp])."""
+    import os
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    for p in (here, root, os.path.join(root, "senquential-convex-programming-for-trajectory-planning_amd")):
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    from oracle import scp_reference as R_
+    n_veh, hp, x0, u0, ec = args[:5]
+    sc = R_.circle_scenario(n_veh, Hp=args[5] if len(args) > 5 else hp)
+    p = R_.make_problem(sc, x0, u0, ec, Hp=hp)
+    return R_.scp_solve(p, mode="structured", keep_history=True)

@@ -3,13 +3,13 @@
 * c4: 4 vehicles x 65536 realisations over 8 GPUs = 8192 problems per rank.  One
   full rank shard (rank 7: global problems 57344..65535, inputs generated from the
   global index as bench.py does) runs in one launch; size-independent properties on
-  every problem, oracle parity (per SCP iteration on a stop flip) on 16 of them.
+  every problem, oracle parity (per SCP iteration on a stop flip) on 64 of them.
 * c3: 8 vehicles, Hp 30, B = 4096 (the LDS-pressure configuration); the same
-  properties on all problems and oracle parity on 8 problems spread over the batch.
+  properties on all problems and oracle parity on 32 problems spread over the batch.
 * c5: 4 vehicles, mixed horizons Hp in {10, 20, 30} (problem g gets Hp[g mod 3]),
   B = 3072 in hp_max = 30 slots (the divergent-wavefront stress configuration, per
   problem early exit, SCP_controller.py:191-195); the properties on every problem
-  and per-iteration oracle parity on 6 problems of each horizon class.
+  and per-iteration oracle parity on 12 problems of each horizon class.
 """
 import multiprocessing as mp
 
@@ -27,19 +27,7 @@ import scp_parity as SP
 pytestmark = pytest.mark.gpu
 
 
-def _oracle_job(args):
-    import os
-    import sys
-    here = os.path.dirname(os.path.abspath(__file__))
-    root = os.path.dirname(here)
-    for p in (here, root, os.path.join(root, "senquential-convex-programming-for-trajectory-planning_amd")):
-        if p not in sys.path:
-            sys.path.insert(0, p)
-    from oracle import scp_reference as R_
-    n_veh, hp, x0, u0, ec = args[:5]
-    sc = R_.circle_scenario(n_veh, Hp=args[5] if len(args) > 5 else hp)
-    p = R_.make_problem(sc, x0, u0, ec, Hp=hp)
-    return R_.scp_solve(p, mode="structured", keep_history=True)
+_oracle_job = SP.oracle_job
 
 
 def _properties(S, sc, bt, out, nV, Hp, hp=None):
@@ -90,7 +78,7 @@ def test_c4_rank_shard_8192(gpu):
     o2 = S.solve(sub.x0, sub.u0, sub.ec_noise)
     torch.cuda.synchronize()
     assert torch.equal(o2.u, out.u[4096:4096 + 64])
-    idx = list(range(0, per_rank, per_rank // 16))
+    idx = list(range(0, per_rank, per_rank // 64))
     _parity(out, bt, idx, 4, 20, workers=16)
     S.close()
 
@@ -104,8 +92,8 @@ def test_c3_full_batch_4096(gpu):
     torch.cuda.synchronize()
     conv = _properties(S, sc, bt, out, 8, 30)
     assert conv >= 0.8          # the reference's own 20-QP cap binds for ~12 % at c3
-    idx = list(range(0, B, B // 8))
-    _parity(out, bt, idx, 8, 30, workers=8)
+    idx = list(range(0, B, B // 32))
+    _parity(out, bt, idx, 8, 30, workers=16)
     S.close()
 
 
@@ -124,8 +112,8 @@ def test_c5_mixed_horizon_full_batch_3072(gpu):
     for H in (10, 20):
         sel = bt.hp == H
         assert np.all(u[sel, 4 * H:] == 0.0)
-    # per-iteration parity: 6 problems of each horizon class, spread over the batch
-    idx = [b for H in Hs for b in np.flatnonzero(bt.hp == H)[::B // 3 // 6][:6].tolist()]
+    # per-iteration parity: 12 problems of each horizon class, spread over the batch
+    idx = [b for H in Hs for b in np.flatnonzero(bt.hp == H)[::B // 3 // 12][:12].tolist()]
     jobs = [(4, int(bt.hp[b]), bt.x0[b], bt.u0[b], bt.ec_noise[b], 30) for b in idx]
     with mp.get_context("spawn").Pool(16) as pool:
         res = pool.map(_oracle_job, jobs)
