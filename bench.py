@@ -20,9 +20,10 @@ starts the N rank processes itself, one per GPU, before anything touches a GPU
 Prints ONE JSON line (rank 0).  ``roofline`` prices the dominant (only)
 kernel against the FP64 peak with the algorithmic FLOP count of the executed
 algorithm (scpqp/flops.py); ``cpu_baseline`` times the in-repo CPU
-restatement of the reference path (oracle/, faithful mode) on a bounded sample
-of the same problems on the host cores, and ``traj_linf_err`` is the GPU-vs-
-oracle trajectory error on that sample.
+restatement of the reference path (oracle/: faithful mode = the reference CPU
+path, and structured mode = the optimised CPU path, each at the all-core and the
+1-core rate) on a bounded sample of the same problems on the host cores, and
+``traj_linf_err`` is the GPU-vs-oracle trajectory error on that sample.
 """
 from __future__ import annotations
 
@@ -43,47 +44,62 @@ import numpy as np  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD datasheet
 HBM_PEAK_GBS = 8000.0
 METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
-# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu_measure.sh + pmc_summary.py)
+# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu.sh pmc + pmc_summary.py)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic_{}.json")
 PMC_SQ = os.path.join(ROOT, "profiles", "r04_pmc_sq_{}.json")
 
 
 # ----------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
-    """Spawned worker: the oracle's faithful restatement of the reference path."""
+    """Spawned worker: the oracle's restatement of the reference path in one mode,
+    single-threaded.  faithful = the dense QCQP_formulate tensors of
+    SCP_controller.py:278-341 (the named "reference CPU path"); structured = the
+    factored rows of SURVEY A.5 (the optimised CPU path)."""
     os.environ.setdefault("OMP_NUM_THREADS", "1")
     sys.path.insert(0, ROOT)
     from oracle import scp_reference as R
-    n_veh, hps, x0s, u0s, ecs = args
+    n_veh, mode, hps, x0s, u0s, ecs = args
     sc = R.circle_scenario(n_veh, Hp=int(max(hps)))
     out = []
     t0 = time.perf_counter()
     for x0, u0, ec, hp in zip(x0s, u0s, ecs, hps):
         p = R.make_problem(sc, x0, u0, ec, Hp=int(hp))
-        # faithful (dense QCQP_formulate tensors) up to 4 vehicles; at 8 vehicles, Hp 30 the
-        # dense Phi is 774 MB per problem, so the structured restatement is timed instead
-        r = R.scp_solve(p, mode="faithful" if n_veh <= 4 else "structured")
+        r = R.scp_solve(p, mode=mode)
         out.append((r.traj, r.n_scp, r.converged))
     return time.perf_counter() - t0, out
 
 
-def cpu_baseline(bt, n_veh, sample, workers):
+def cpu_modes(n_veh):
+    """Oracle modes timed by the CPU leg, the reference CPU path first.  At 8 vehicles,
+    Hp 30 the dense Phi of the faithful mode is 774 MB per problem, so only the
+    structured mode is timed there."""
+    return ("faithful", "structured") if n_veh <= 4 else ("structured",)
+
+
+def cpu_baseline(bt, n_veh, sample, workers, mode):
+    """All-core leg: `sample` problems over `workers` spawned single-threaded processes.
+    Returns (wall seconds, summed worker seconds, per-problem results)."""
     idx = np.arange(sample)
     chunks = [c for c in np.array_split(idx, workers) if len(c)]
-    jobs = [(n_veh, bt.hp[c], bt.x0[c], bt.u0[c], bt.ec_noise[c]) for c in chunks]
+    jobs = [(n_veh, mode, bt.hp[c], bt.x0[c], bt.u0[c], bt.ec_noise[c]) for c in chunks]
     ctx = mp.get_context("spawn")
     env_keep = os.environ.get("OMP_NUM_THREADS")
     os.environ["OMP_NUM_THREADS"] = "1"
     os.environ["OPENBLAS_NUM_THREADS"] = "1"
-    t0 = time.perf_counter()
     with ctx.Pool(len(jobs)) as pool:
+        pool.map(_noop, range(len(jobs)))   # interpreter start-up outside the timed region
+        t0 = time.perf_counter()
         res = pool.map(_cpu_worker, jobs)
-    wall = time.perf_counter() - t0
+        wall = time.perf_counter() - t0
     if env_keep is not None:
         os.environ["OMP_NUM_THREADS"] = env_keep
     cpu_s = sum(r[0] for r in res)
     trajs = [t for r in res for t in r[1]]
     return wall, cpu_s, trajs
+
+
+def _noop(_):
+    return 0
 
 
 def pmc_traffic(tj):
@@ -109,11 +125,48 @@ def roofline_bound(sq, flops):
     return "fp64-valu", f"MFMA carries {share:.0%} of the executed FP64 FLOPs (VALU FMA pipe)"
 
 
-def cpu_leg(bt, n_veh, cpu_sample, B):
-    cores = host_cores()
+def cpu_leg(bt, n_veh, cpu_sample, B, cores=None):
+    """Time every oracle mode of cpu_modes() on the same bounded sample.  Per mode:
+    wall (all cores) and cpu_s (summed single-thread worker seconds, so sample / cpu_s
+    is the 1-core rate).  The first mode's trajectories are the parity sample."""
+    cores = cores or host_cores()
     sample = min(cpu_sample, B)
-    wall, cpu_s, cpu_trajs = cpu_baseline(bt, n_veh, sample, cores)
-    return dict(wall=wall, cpu_s=cpu_s, trajs=cpu_trajs, cores=cores, sample=sample)
+    modes = {}
+    trajs = None
+    for mode in cpu_modes(n_veh):
+        wall, cpu_s, tr = cpu_baseline(bt, n_veh, sample, cores, mode)
+        modes[mode] = dict(wall=wall, cpu_s=cpu_s)
+        trajs = tr if trajs is None else trajs
+    first = modes[cpu_modes(n_veh)[0]]
+    return dict(wall=first["wall"], cpu_s=first["cpu_s"], modes=modes, trajs=trajs, cores=cores,
+                sample=sample)
+
+
+def cpu_baseline_block(cpu, config, n_veh):
+    """The bench line's cpu_baseline: `value` is the reference CPU path (the first mode)
+    on all cores; the structured (optimised CPU) mode and the 1-core rates beside it."""
+    modes = cpu["modes"]
+    ref = cpu_modes(n_veh)[0]
+    n = cpu["sample"]
+    blk = {
+        "value": n / modes[ref]["wall"], "unit": "SCP solves/s", "cores": cpu["cores"],
+        "kind": "port",
+        "mode": ref,
+        "value_1core": n / modes[ref]["cpu_s"],
+        "value_structured": n / modes["structured"]["wall"],
+        "value_structured_1core": n / modes["structured"]["cpu_s"],
+        "sample": f"first {n} problems of the same {config} batch, oracle "
+                  + ("faithful mode (dense QCQP_formulate tensors" if ref == "faithful"
+                     else "structured mode (factored rows; the dense Phi is 774 MB per problem")
+                  + f", scipy expm, dense IPM + exact polish), {cpu['cores']} spawned "
+                  f"single-threaded workers; " + ", ".join(
+                      f"{m}: {v['cpu_s']:.1f} s of CPU work, {v['wall']:.2f} s wall"
+                      for m, v in modes.items()),
+        "note": "value / value_structured: all cores (sample / wall); *_1core: one core "
+                "(sample / summed single-thread worker seconds); structured = factored "
+                "constraint rows (SURVEY A.5), the optimised CPU path",
+    }
+    return blk
 
 
 def cpu_leg_dump(cpu, path):
@@ -329,7 +382,7 @@ def main():
     value = world * B * args.steps / elapsed
 
     # HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes of this
-    # workload at its default batch (tools/gpu_measure.sh + tools/pmc_summary.py)
+    # workload at its default batch (tools/gpu.sh pmc + tools/pmc_summary.py)
     traffic, traffic_raw, sq = None, None, None
     default_b = {"c2": 1024, "c3": 4096, "c4": 8192, "c5": 3072}[args.config]
     tpath = PMC_TRAFFIC.format(args.config)
@@ -421,15 +474,7 @@ def main():
                 mine = trajs[b].reshape(-1)[:H * 2 * args.n_veh].reshape(H, 2, args.n_veh)
                 e = float(np.abs(mine - tr).max())
                 (errs if conv and (status[b] & 0xff) == 0 else capped).append(e)
-        line["cpu_baseline"] = {
-            "value": cpu["sample"] / cpu["wall"], "unit": "SCP solves/s", "cores": cpu["cores"],
-            "kind": "port",
-            "sample": f"first {cpu['sample']} problems of the same {args.config} batch, oracle "
-                      f"{'faithful mode (dense QCQP_formulate tensors' if args.n_veh <= 4 else 'structured mode (factored rows'}"
-                      f", scipy expm, dense IPM + exact polish), "
-                      f"{cpu['cores']} spawned single-threaded workers; "
-                      f"{cpu['cpu_s']:.1f} s of CPU work",
-        }
+        line["cpu_baseline"] = cpu_baseline_block(cpu, args.config, args.n_veh)
         line["traj_linf_err"] = max(errs) if errs else None
         line["traj_err_reference"] = ("in-repo CPU restatement of the reference path (oracle/; "
                                       "CVXOPT/GUROBI absent, parity unpinned: SURVEY 8c)")

@@ -128,9 +128,11 @@ typedef struct scpqp_batch_out {
                                   [0] delta  [1] obj  [2] max_violation  [3] sum_violations
                                   [4] slack omega = z[N]  [5] IPM iterations of this QP
                                   [6] QP flags (1 certified, 2 warm-started)  [7] feasible
-                                  [8, 8+N)        u_lin: the iterate the rows linearise at
-                                  [8+N, 8+2N)     u: this QP's solution z[:N]
-                                  [8+2N, 8+2N+4m) rows r: e_r[0], e_r[1], w_r, h_r (scaled
+                                  [8] obj_0 + 1e5 max_violation_0, the merit before this
+                                      iteration (delta_hat = [8] - fval, :159)  [9] 0
+                                  [10, 10+N)        u_lin: the iterate the rows linearise at
+                                  [10+N, 10+2N)     u: this QP's solution z[:N]
+                                  [10+2N, 10+2N+4m) rows r: e_r[0], e_r[1], w_r, h_r (scaled
                                                   factored row, SURVEY A.5); Aineq/bineq
                                                   follow as A_r = -(e_r.g) nrm/uLim,
                                                   b_r = h_r nrm, nrm = -1/w_r

@@ -36,6 +36,7 @@ import functools
 import time
 
 import numpy as np
+import torch
 
 from Config import Config
 from MPC_Iter import MPCclass
@@ -69,6 +70,10 @@ class _LazyLog(dict):
     def __eq__(self, other):
         self._fill()
         return super().__eq__(other)
+
+    def __ne__(self, other):
+        self._fill()
+        return super().__ne__(other)
 
     __hash__ = None
 
@@ -139,9 +144,9 @@ def _iteration_log(trace, n_scp, nV, nO, Hp, hp_max, u_lim, Mb, const_term, Phi_
       (:117-127; the same arrays every iteration, as the reference appends them);
     * Aineq / bineq: dense rows from the factored ones and the Toeplitz blocks (:93-128);
     * x = [u; slack], SCP_ObjVal = fval = 1/2 x'Px + q'x + gamma0 (:146, :158);
-    * delta_hat = (obj_0 + 1e5 maxviol_0) - fval (:159), where obj_0 + 1e5 maxviol_0 is
-      the previous evaluation's, recovered from the recorded delta = that - (obj + 1e5
-      maxviol) (:160);
+    * slack = x[-1] as a shape-(1,) array, like the reference's u_var[-1] (:148);
+    * delta_hat = (obj_0 + 1e5 maxviol_0) - fval (:159), with the merit obj_0 + 1e5
+      maxviol_0 before the iteration as the kernel recorded it (trace header [8]);
     * Traj / U, prevTraj / prevU: forward_U of u and of the linearisation point (:183-187):
       positions const_term + Mathcal_B u, U = u per vehicle [Hp, nu, nVeh]."""
     from scpqp import trace as TR
@@ -173,7 +178,6 @@ def _iteration_log(trace, n_scp, nV, nO, Hp, hp_max, u_lim, Mb, const_term, Phi_
     for d in its:
         uu = d['z'][:-1]
         fval = float(uu @ Phi0 @ uu + Psi0 @ uu + SLACK_WEIGHT * d['slack'] + gamma0)
-        prev_merit = d['delta'] + d['obj'] + SLACK_WEIGHT * d['maxviol']
         log['P'].append(P)
         log['q'].append(q)
         log['Aineq'].append(d['A'])
@@ -181,10 +185,10 @@ def _iteration_log(trace, n_scp, nV, nO, Hp, hp_max, u_lim, Mb, const_term, Phi_
         log['lb'].append(lb)
         log['ub'].append(ub)
         log['x'].append(d['z'].reshape(-1, 1))
-        log['slack'].append(d['slack'])
+        log['slack'].append(np.array([d['slack']]))
         log['SCP_ObjVal'].append(fval)
         log['QCQP_ObjVal'].append(np.array([[d['obj']]]))
-        log['delta_hat'].append(prev_merit - fval)
+        log['delta_hat'].append(d['merit0'] - fval)
         log['delta'].append(d['delta'])
         log['u'].append(uu.reshape(-1, 1))
         log['feasible'].append(d['feasible'])
@@ -251,13 +255,18 @@ class SCPcontroller:
             u_approx[0] = np.spacing(1)
         res = self.solver.solve(u_warm=np.asarray(u_approx, float).reshape(1, -1), trace=True,
                                 **self._inputs())
+        # the trace goes to pinned host memory asynchronously, queued before the copies
+        # below (same stream), which therefore return with it complete: the log costs one
+        # queued copy inside optimizerTime, and its decode runs only when the log is read
+        tr_host = torch.empty(res.trace.shape[1:], dtype=res.trace.dtype, pin_memory=True)
+        tr_host.copy_(res.trace[0], non_blocking=True)
         u = res.u[0, :self.nVeh * self.Hp].cpu().numpy().reshape(-1, 1)
         status = int(res.status[0].item())
         n_scp = int(res.n_scp[0].item())
         m = self.mpc
         # the decode's inputs, host arrays only (the trace rows of this solve and the
         # linearisation): the log keeps neither the controller nor device tensors alive
-        dec = functools.partial(_iteration_log, res.trace[0, :n_scp].cpu().numpy(), n_scp,
+        dec = functools.partial(_iteration_log, tr_host.numpy()[:n_scp], n_scp,
                                 self.nVeh, self.nObst, self.Hp, self.solver.hp_max,
                                 self.scenario_uLim, m.Mathcal_B.copy(), m.const_term.copy(),
                                 m.Phi_0.copy(), m.Psi_0.copy(), float(np.sum(m.gamma_0)))

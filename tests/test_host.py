@@ -203,13 +203,42 @@ def test_bench_cpu_leg_round_trip(tmp_path):
     sys.path.insert(0, ROOT)
     import bench
     cpu = dict(wall=1.5, cpu_s=3.0, cores=2, sample=2,
+               modes={"faithful": dict(wall=1.5, cpu_s=3.0), "structured": dict(wall=1.0, cpu_s=2.0)},
                trajs=[(np.arange(6.0).reshape(3, 2), 5, True), (np.ones((3, 2)), 20, False)])
     path = str(tmp_path / "cpu.json")
     bench.cpu_leg_dump(cpu, path)
     back = bench.cpu_leg_load(path)
     assert back["wall"] == 1.5 and back["cores"] == 2 and back["sample"] == 2
+    assert back["modes"]["structured"]["cpu_s"] == 2.0
     for (t0, n0, c0), (t1, n1, c1) in zip(cpu["trajs"], back["trajs"]):
         assert np.array_equal(t0, t1) and n0 == n1 and c0 == c1
+
+
+def test_bench_cpu_baseline_fields_on_a_sample():
+    """SURVEY 8(d)'s CPU leg on a 4-problem c2 sample: the reference CPU path (faithful
+    mode) and the structured mode, each at the all-core and the 1-core rate, on the same
+    problems, and the faithful trajectories are the parity sample."""
+    sys.path.insert(0, ROOT)
+    import bench
+    from scpqp import shard
+    sc = _circle(4, hp=20)
+    bt = shard.shard_batch(sc, 8, 0, base_seed=0)
+    cpu = bench.cpu_leg(bt, 4, 4, 8, cores=2)
+    assert cpu["sample"] == 4 and cpu["cores"] == 2 and len(cpu["trajs"]) == 4
+    assert set(cpu["modes"]) == {"faithful", "structured"}
+    blk = bench.cpu_baseline_block(cpu, "c2", 4)
+    for k in ("value", "value_1core", "value_structured", "value_structured_1core"):
+        assert np.isfinite(blk[k]) and blk[k] > 0, k
+    m = cpu["modes"]
+    assert blk["value"] == pytest.approx(4 / m["faithful"]["wall"])
+    assert blk["value_1core"] == pytest.approx(4 / m["faithful"]["cpu_s"])
+    assert blk["value_structured_1core"] == pytest.approx(4 / m["structured"]["cpu_s"])
+    assert blk["mode"] == "faithful" and blk["cores"] == 2 and blk["kind"] == "port"
+    # two workers: the all-core rate exceeds the 1-core rate (up to start-up noise)
+    assert blk["value"] > 0.8 * blk["value_1core"]
+    for t, ns, conv in cpu["trajs"]:
+        assert t.shape == (20, 2, 4) and 1 <= ns <= 20
+    assert bench.cpu_modes(8) == ("structured",)
 
 
 def _lazy_log_counter():
@@ -236,6 +265,17 @@ def test_lazy_log_copy_and_pickle_decode_first():
     assert back["x"][0].shape == (3, 1) and back["status"] == 0
     assert copy.copy(log)["delta"] == [0.5] and copy.deepcopy(log)["n_scp"] == 1
     assert log.pop("delta") == [0.5] and len(calls) == 1
+    # != decodes first as well: it agrees with not ==
+    calls2 = []
+
+    def dec2():
+        calls2.append(1)
+        return {"delta": [0.5]}
+    log2 = SC._LazyLog({"status": 0, "n_scp": 1}, dec2)
+    assert (log2 != {"status": 0, "n_scp": 1}) and len(calls2) == 1
+    full = {"status": 0, "n_scp": 1, "delta": [0.5]}
+    log3 = SC._LazyLog({"status": 0, "n_scp": 1}, lambda: {"delta": [0.5]})
+    assert not (log3 != full) and log3 == full
 
 
 def test_iteration_log_keys_and_formulas():
@@ -271,8 +311,8 @@ def test_iteration_log_keys_and_formulas():
         x = log["x"][it].reshape(-1)
         fval = 0.5 * x @ log["P"][it] @ x + log["q"][it].reshape(-1) @ x + 2.5
         assert log["SCP_ObjVal"][it] == pytest.approx(fval, rel=1e-12)
-        merit = tr[it, 0] + tr[it, 1] + 1e5 * tr[it, 2]
-        assert log["delta_hat"][it] == pytest.approx(merit - fval, rel=1e-12)
+        assert log["delta_hat"][it] == pytest.approx(tr[it, 8] - fval, rel=1e-12)
+        assert log["slack"][it].shape == (1,) and log["slack"][it][0] == tr[it, 4]
         u = log["u"][it].reshape(-1)
         for v in range(nV):
             X = (const_term[:, :, v] + Mb[:, :, v] @ u[v * Hp:(v + 1) * Hp, None]).reshape(2, Hp, order="F")

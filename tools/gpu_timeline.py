@@ -18,7 +18,7 @@ from scpqp import _lib as LB  # noqa: E402
 from scpqp import batch as BT  # noqa: E402
 from scpqp.solver import ScpQpSolver  # noqa: E402
 
-lib = LB.load(os.path.join(PKG, "scpqp", "libscpqp_prof.so"))
+lib = LB.load(os.environ.get("SCPQP_PROF_LIB") or os.path.join(PKG, "scpqp", "libscpqp_prof.so"))
 LB._lib = lib
 lib.scpqp_prof_times.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1024

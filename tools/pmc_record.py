@@ -1,5 +1,5 @@
 """Build the per-config SQ counter record bench.py reads (profiles/rNN_pmc_sq_<cfg>.json)
-from tools/gpu_measure.sh's pmc_sq_<cfg>.txt and pmc_mfma_<cfg>.txt (tools/pmc_table.py output).
+from tools/gpu.sh pmc's pmc_sq_<cfg>.txt and pmc_mfma_<cfg>.txt (tools/pmc_table.py output).
 
     python tools/pmc_record.py <measure dir> <cfg> <kernel label> <session tag> > profiles/r03_pmc_sq_<cfg>.json
 """
@@ -39,7 +39,7 @@ def main():
         "mfma_busy_cycles_per_inst": busy / mfma if mfma else None,
         "note": (f"rocprofv3 --kernel-trace --pmc, one 8-counter SQ pass and one MFMA/VALU pass, "
                  f"bench.py --config {cfg} --steps 2 --warmup 1 --no-cpu; per-dispatch means "
-                 f"(tools/pmc_table.py), shipped library (tools/gpu_measure.sh {tag})"),
+                 f"(tools/pmc_table.py), shipped library (tools/gpu.sh pmc {tag})"),
     }
     json.dump(rec, sys.stdout, indent=1)
 
