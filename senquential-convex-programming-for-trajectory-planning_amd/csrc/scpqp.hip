@@ -360,12 +360,22 @@ __device__ __forceinline__ double wave_max(double v) { return wave_reduce<true>(
 
 // Reduce four values across the workgroup; bit q of maxmask: max, else sum.
 // NQ: number of leading slots in use (the rest are left untouched).
-template <int NQ = 4>
+// BUF: which of two 16-slot buffers (red[0, 16) or red[16, 32)) carries the partial
+// sums.  One barrier (round 5; two before): a wave may write its partials while a
+// slower wave still reads the previous reduction's, so two reductions that follow each
+// other with no barrier between them use different buffers (DESIGN §3 lists the pairs).
+#ifdef SCPQP_REDUCE2
+#define REDUCE_FIRST_BARRIER 1
+#else
+#define REDUCE_FIRST_BARRIER 0
+#endif
+template <int NQ = 4, int BUF = 0>
 __device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldouble* red) {
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    red += 16 * BUF;
 #pragma unroll
     for (int q = 0; q < NQ; ++q) v[q] = (maxmask >> q & 1) ? wave_max(v[q]) : wave_sum(v[q]);
-    __syncthreads();
+    if (REDUCE_FIRST_BARRIER) __syncthreads();
     if (l == 0) {
 #pragma unroll
         for (int q = 0; q < NQ; ++q) red[w * 4 + q] = v[q];
@@ -910,7 +920,25 @@ __device__ __forceinline__ double gx_row(const LT& L, PX xu, double xw, int r) {
     return -xw;
 }
 
-// G' t: u-part into out[0..N), omega part returned (uniform).
+// G' t: fin(e, (G't)_e) for the u-part e < N (in the thread that owns e), omega part
+// returned (uniform).  No barrier after the u-part: the caller's next barrier publishes it.
+template <class LT, class PT, class Fin>
+__device__ double gt_apply_fin(const LT& L, PT t, Fin fin) {
+    const int tid = threadIdx.x;
+    double wsum = 0.0;
+    for (int e = tid; e < L.V * L.Hb; e += NT) {
+        const int v = e / L.Hb, k = e % L.Hb;
+        double s0, s1;
+        incident_sum(L, v, k, [&](int r) { return t[r]; }, s0, s1);
+        L.yb[2 * e] = s0;
+        L.yb[2 * e + 1] = s1;
+    }
+    for (int r = tid; r < L.m; r += NT) wsum += t[r] * L.rowW[r];
+    double red[4] = {wsum, 0.0, 0.0, 0.0};
+    block_reduce4<1>(red, 0, L.red);   // barrier: yb visible afterwards
+    toeplitz_t_apply(L, L.yb, [&](int e, double tt) { fin(e, tt + t[L.m + e] - t[L.m + L.N + e]); });
+    return red[0] - t[L.mc - 1];
+}
 template <class LT, class PT, class PO>
 __device__ double gt_apply(const LT& L, PT t, PO out) {
     const int tid = threadIdx.x;
@@ -1091,21 +1119,25 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     double ww = 0.0;
     for (int r = tid; r < L.m; r += NT) ww += d[r] * L.rowW[r] * L.rowW[r];
     double red[4] = {ww, 0.0, 0.0, 0.0};
-    block_reduce4<1>(red, 0, L.red);
+    block_reduce4<1, 1>(red, 0, L.red);   // may follow ph_polish_accept's (buffer 0)
     PROF_ACC_FINE0(25);
     // phase 2: K_uu lower triangle in TS x TS tiles (assemble_tiles); 4 x 4 where
     // there are enough of them to give every thread two (only the workspace plans
     // have such horizons: the LDS-plan kernels do not carry the 4 x 4 registers)
     const int T4 = (Hb + 3) >> 2, PV = V * (V - 1) / 2;
+    // LDS factors (c2, c5) take the 4 x 4 tiles too since round 5: at c2 the 210 tiles
+    // leave 46 of 256 threads idle, but each trip serves 16 entries for the same four
+    // loads, and the busiest thread does 20 trips instead of 32 (c2 +0.6 %, c4 +1.9 %,
+    // scratch 196 -> 236 B per lane)
     if constexpr (LT::HGLOBAL) {
         if (V * (T4 * (T4 + 1) / 2) + PV * T4 * T4 >= 2 * NT) assemble_tiles<4>(P, L, d, rho);
         else assemble_tiles<2>(P, L, d, rho);
     } else {
         (void)T4;
         (void)PV;
-        assemble_tiles<2>(P, L, d, rho);
+        assemble_tiles<4>(P, L, d, rho);
 #ifdef SCPQP_DIAG_X2_ASM   // counter attribution: the tiles again (the same values stored)
-        assemble_tiles<2>(P, L, d, rho);
+        assemble_tiles<4>(P, L, d, rho);
 #endif
     }
     PROF_ACC_FINE0(26);
@@ -2137,25 +2169,11 @@ __device__ void residuals(const cParams& P, const LT& L, double (&out)[4]) {
     const double rdw = P.slackW + red[2] - L.lam[L.mc - 1];
     if (tid == 0) L.rd[N] = rdw;
     double red2[4] = {mrd, quad2, lin, 0.0};
-    block_reduce4<3>(red2, 1, L.red);
+    block_reduce4<3, 1>(red2, 1, L.red);
     out[0] = red[0];
     out[1] = fmax(red2[0], fabs(rdw));
     out[2] = red[1];
     out[3] = 0.5 * (red[3] + red2[1]) + red2[2] + P.slackW * zw;
-}
-
-// max step keeping s + a ds >= 0, lam + a dl >= 0 (capped at 1)
-template <class LT>
-__device__ double max_step(const LT& L) {
-    double a = 1.0;
-    for (int r = threadIdx.x; r < L.mc; r += NT) {
-        // v_rcp_f64 + Newton instead of the IEEE division sequence (per row, every step)
-        if (L.ds[r] < 0.0) a = fmin(a, -L.s[r] * recip(L.ds[r]));
-        if (L.dl[r] < 0.0) a = fmin(a, -L.lam[r] * recip(L.dl[r]));
-    }
-    double red[4] = {-a, 0.0, 0.0, 0.0};
-    block_reduce4<1>(red, 1, L.red);
-    return -red[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -2239,10 +2257,8 @@ PHASE D4 ph_residuals(Ctx c) {
 // rhs = -q + G'(tv) with tv = h (init) or tv = mask (h/delta - y) (polish), + rho x_k
 template <class LT>
 __device__ __forceinline__ void rhs_from_tv_body(const cParams& P, const LT& L, double rho) {
-    const double ow = gt_apply(L, L.tv, L.rhs);
+    const double ow = gt_apply_fin(L, L.tv, [&](int e, double g) { L.rhs[e] = g - L.qs[e] + rho * L.dz[e]; });
     if (threadIdx.x == 0) L.rhs[L.N] = ow - P.slackW + rho * L.dz[L.N];
-    __syncthreads();
-    for (int e = threadIdx.x; e < L.N; e += NT) L.rhs[e] = L.rhs[e] - L.qs[e] + rho * L.dz[e];
     __syncthreads();
 }
 PHASE void ph_rhs_from_tv(Ctx c, double rho) {
@@ -2298,7 +2314,7 @@ PHASE void ph_init_b(Ctx c) {
         smax = fmax(smax, sv);
     }
     double red2[4] = {-smin, smax, 0.0, 0.0};
-    block_reduce4<2>(red2, 3, L.red);
+    block_reduce4<2, 1>(red2, 3, L.red);
     const double ts = fmax(1.5 * red2[0], 0.0);
     const double fl = 0.1 * fmax(1.0, red2[1] + ts);
     const double lam0 = 0.3 * P.slackW / mc;
@@ -2323,27 +2339,38 @@ __device__ __forceinline__ void newton_rhs_body(const LT& L, int corr, double sm
         L.tv[r] = L.dd[r] * L.rp[r] - rc * recip(L.s[r]);
     }
     __syncthreads();
-    const double ow = gt_apply(L, L.tv, L.rhs);
-    if (threadIdx.x == 0) L.rhs[L.N] = ow;
-    __syncthreads();
-    for (int e = threadIdx.x; e < L.n; e += NT) L.rhs[e] = -L.rd[e] - L.rhs[e];
+    const double ow = gt_apply_fin(L, L.tv, [&](int e, double g) { L.rhs[e] = -L.rd[e] - g; });
+    if (threadIdx.x == 0) L.rhs[L.N] = -L.rd[L.N] - ow;
     __syncthreads();
 }
+// ds = -rp - G dz row by row in the thread that forms (G dz)_r, and this thread's
+// partial step lengths {primal: min over ds < 0 of -s/ds, dual: min over dl < 0 of
+// -lam/dl} from the values it just formed (round 5: one barrier and one pass over the
+// rows fewer than G dz, the direction and the ratio tests apart; the same operations).
 template <class LT>
-__device__ __forceinline__ void newton_back_body(const LT& L, int corr, double smu) {
-    g_apply(L, L.dz, L.ds, false);
+__device__ __forceinline__ double2v newton_back_body(const LT& L, int corr, double smu) {
+    toeplitz_apply(L, L.dz, L.ya);
+    __syncthreads();
+    const double xw = L.dz[L.N];
+    double ap = 1.0, ad = 1.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
-        const double dsr = -L.rp[r] - L.ds[r];
+        const double dsr = -L.rp[r] - gx_row(L, L.dz, xw, r);
+        const double dlr = -(rc + L.lam[r] * dsr) * recip(L.s[r]);
         L.ds[r] = dsr;
-        L.dl[r] = -(rc + L.lam[r] * dsr) * recip(L.s[r]);
+        L.dl[r] = dlr;
+        if (dsr < 0.0) ap = fmin(ap, -L.s[r] * recip(dsr));
+        if (dlr < 0.0) ad = fmin(ad, -L.lam[r] * recip(dlr));
     }
     __syncthreads();
+    return double2v{ap, ad};
 }
 // predictor step length and Mehrotra centring: returns sigma * mu; stores the affine direction
 template <class LT>
-__device__ __forceinline__ double affine_body(const LT& L, double mu) {
-    const double aaff = max_step(L);
+__device__ __forceinline__ double affine_body(const LT& L, double mu, double2v part) {
+    double redm[4] = {-fmin(part.x, part.y), 0.0, 0.0, 0.0};
+    block_reduce4<1>(redm, 1, L.red);   // = max_step(L)
+    const double aaff = -redm[0];
     double mua = 0.0;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
         mua += (L.s[r] + aaff * L.ds[r]) * (L.lam[r] + aaff * L.dl[r]);
@@ -2351,7 +2378,7 @@ __device__ __forceinline__ double affine_body(const LT& L, double mu) {
         L.la[r] = L.dl[r];
     }
     double red[4] = {mua, 0.0, 0.0, 0.0};
-    block_reduce4<1>(red, 0, L.red);
+    block_reduce4<1, 1>(red, 0, L.red);   // follows max_step's (buffer 0)
     const double sr = red[0] / L.mc / mu;
     return sr * sr * sr * mu;
 }
@@ -2362,13 +2389,9 @@ __device__ __forceinline__ double affine_body(const LT& L, double mu) {
 // Hp 30 11.0 -> 10.1, c3 14.0 -> 13.1 (max 23 -> 19), frog 15.9 -> 11.0; Hp 10 and
 // parallel5 unchanged; every polish certifies the same minimiser.
 template <class LT>
-__device__ __forceinline__ void update_body(const LT& L, double eta) {
+__device__ __forceinline__ void update_body(const LT& L, double eta, double2v part) {
     // separate step lengths: (z, s) by the primal ratio test, lam by the dual one
-    double ap = 1.0, ad = 1.0;
-    for (int r = threadIdx.x; r < L.mc; r += NT) {
-        if (L.ds[r] < 0.0) ap = fmin(ap, -L.s[r] * recip(L.ds[r]));
-        if (L.dl[r] < 0.0) ad = fmin(ad, -L.lam[r] * recip(L.dl[r]));
-    }
+    double ap = part.x, ad = part.y;
     double red[4] = {-ap, -ad, 0.0, 0.0};
     block_reduce4<2>(red, 3, L.red);
     ap = fmin(1.0, eta * -red[0]);
@@ -2420,8 +2443,8 @@ PHASE void ph_init_assemble_factor(Ctx c) {
 // predictor back-substitution, affine step and centring, corrector right-hand side
 PHASE double ph_back_affine_rhs(Ctx c, double mu) {
     LAYDEF;
-    newton_back_body(L, 0, 0.0);
-    const double smu = affine_body(L, mu);
+    const double2v part = newton_back_body(L, 0, 0.0);
+    const double smu = affine_body(L, mu, part);
     newton_rhs_body(L, 1, smu);
     return smu;
 }
@@ -2429,8 +2452,8 @@ PHASE double ph_back_affine_rhs(Ctx c, double mu) {
 // point (the next iteration's convergence test)
 PHASE D4 ph_back_update_residuals(Ctx c, double smu, double eta) {
     LAYDEF;
-    newton_back_body(L, 1, smu);
-    update_body(L, eta);
+    const double2v part = newton_back_body(L, 1, smu);
+    update_body(L, eta, part);
     double r[4];
     residuals(P, L, r);
     return D4{r[0], r[1], r[2], r[3]};
@@ -2489,15 +2512,21 @@ PHASE void ph_polish_rhs(Ctx c) {
 template <class LT>
 __device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
     const double idl = L.red[kIdlSlot];
-    g_apply(L, L.dz, L.rp, true);
+    // rp = G x_k - h row by row in the thread that uses it (round 5: one barrier fewer
+    // per multiplier iteration than G x_k - h and the update apart)
+    toeplitz_apply(L, L.dz, L.ya);
+    __syncthreads();
+    const double xw = L.dz[L.N];
     double viol = -1e300, yneg = -1e300;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
+        const double rpr = gx_row(L, L.dz, xw, r) - hval(L, r);
+        L.rp[r] = rpr;
         if (L.sa[r] != 0.0) {
-            const double y = L.la[r] + L.rp[r] * idl;
+            const double y = L.la[r] + rpr * idl;
             L.la[r] = y;
             yneg = fmax(yneg, -y);
         } else {
-            viol = fmax(viol, L.rp[r]);
+            viol = fmax(viol, rpr);
         }
     }
     double dmax = 0.0, xmax = 0.0;
@@ -2538,7 +2567,7 @@ PHASE int ph_polish_accept(Ctx c, double hmax, int converged) {
     for (int e = tid; e < L.n; e += NT)
         if (!isfinite(L.dz[e])) nonfin = 1.0;
     double red[4] = {viol, -ymin, ymax, nonfin};
-    block_reduce4<4>(red, 15, L.red);
+    block_reduce4<4, 1>(red, 15, L.red);   // may follow polish_dual_body's (buffer 0)
     const double vtol = 1e-9 * hmax, ytol = -1e-9 * fmax(1.0, red[2]);
     // a point is certified only if the multiplier iteration has also converged
     // (stationarity), else only the active set is corrected
