@@ -129,7 +129,8 @@ typedef struct scpqp_batch_out {
                                   [4] slack omega = z[N]  [5] IPM iterations of this QP
                                   [6] QP flags (1 certified, 2 warm-started)  [7] feasible
                                   [8] obj_0 + 1e5 max_violation_0, the merit before this
-                                      iteration (delta_hat = [8] - fval, :159)  [9] 0
+                                      iteration (delta_hat = [8] - fval, :159)
+                                  [9] this QP's polish rounds + 4096 x its polish solves
                                   [10, 10+N)        u_lin: the iterate the rows linearise at
                                   [10+N, 10+2N)     u: this QP's solution z[:N]
                                   [10+2N, 10+2N+4m) rows r: e_r[0], e_r[1], w_r, h_r (scaled

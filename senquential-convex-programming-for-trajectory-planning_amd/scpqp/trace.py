@@ -41,7 +41,8 @@ def decode(trace_b, n_iter, nV, nO, H, hp_max, g=None, u_lim=None):
         rows = t[HDR + 2 * Nm:HDR + 2 * Nm + 4 * m].reshape(m, 4)
         d = dict(delta=t[0], obj=t[1], maxviol=t[2], sumviol=t[3], slack=t[4],
                  ipm_iters=int(t[5]), certified=bool(int(t[6]) & 1), warm=bool(int(t[6]) & 2),
-                 feasible=bool(t[7]), merit0=t[8], u_lin=t[HDR:HDR + N].copy(),
+                 feasible=bool(t[7]), merit0=t[8], polish_rounds=int(t[9]) % 4096,
+                 polish_solves=int(t[9]) // 4096, u_lin=t[HDR:HDR + N].copy(),
                  z=np.concatenate([t[HDR + Nm:HDR + Nm + N], t[4:5]]), rows=rows.copy())
         if g is not None:
             d["A"], d["b"] = dense_rows(rows, np.asarray(g, float).reshape(nV, H, 2), nV, nO, H,
