@@ -2137,11 +2137,18 @@ __device__ void residuals(const cParams& P, const LT& L, double (&out)[4]) {
     const double zw = L.z[N];
     double mrp = 0.0, gap = 0.0, wl = 0.0, quad = 0.0;
     for (int r = tid; r < L.mc; r += NT) {
-        const double v = gx_row(L, L.z, zw, r) + L.s[r] - hval(L, r);
+        const double sr = L.s[r], lr = L.lam[r];
+        const double v = gx_row(L, L.z, zw, r) + sr - hval(L, r);
         L.rp[r] = v;
         mrp = fmax(mrp, fabs(v));
-        gap += L.s[r] * L.lam[r];
-        if (r < L.m) wl += L.lam[r] * L.rowW[r];
+        gap += sr * lr;
+        if (r < L.m) wl += lr * L.rowW[r];
+        // the next IPM iteration's weights d = lam / s and predictor vector
+        // tv = d rp - (s lam) / s (round 5: formed here, in the thread that owns row r,
+        // instead of two passes and two barriers of the factorisation phase)
+        const double is = recip(sr), dr = lr * is;
+        L.dd[r] = dr;
+        L.tv[r] = dr * v - (sr * lr) * is;
     }
     for (int e = tid; e < L.V * Hb; e += NT) {
         const int v = e / Hb, k = e % Hb;
@@ -2332,13 +2339,15 @@ PHASE void ph_init_b(Ctx c) {
 //
 // Newton direction, complementarity target rc = s lam (+ ds_aff dl_aff - smu if corr):
 //   rhs = -rd - G'(d rp - rc/s);  dz = K^{-1} rhs;  ds = -rp - G dz;  dl = -(rc + lam ds)/s
-template <class LT>
+template <bool TV = true, class LT>
 __device__ __forceinline__ void newton_rhs_body(const LT& L, int corr, double smu) {
-    for (int r = threadIdx.x; r < L.mc; r += NT) {
-        const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
-        L.tv[r] = L.dd[r] * L.rp[r] - rc * recip(L.s[r]);
+    if constexpr (TV) {   // else tv is already formed (the predictor: residuals())
+        for (int r = threadIdx.x; r < L.mc; r += NT) {
+            const double rc = L.s[r] * L.lam[r] + (corr ? L.sa[r] * L.la[r] - smu : 0.0);
+            L.tv[r] = L.dd[r] * L.rp[r] - rc * recip(L.s[r]);
+        }
+        __syncthreads();
     }
-    __syncthreads();
     const double ow = gt_apply_fin(L, L.tv, [&](int e, double g) { L.rhs[e] = -L.rd[e] - g; });
     if (threadIdx.x == 0) L.rhs[L.N] = -L.rd[L.N] - ow;
     __syncthreads();
@@ -2412,15 +2421,14 @@ __device__ __forceinline__ double step_factor(double mu) { return fmax(0.99, 1.0
 // not need the factor, so it is formed before the factorisation) and L D L' of K in one
 // call (one call fewer per IPM iteration than assembly and factorisation apart: c2 +0.8 %,
 // profiles/r03_ab_fuse_fact.txt).  1 = factored.
+// d and tv come from the residuals of this iterate (residuals()), which every IPM
+// iteration computes last and every IPM pass first.
 PHASE int ph_scale_assemble_rhs_factor(Ctx c) {
     LAYDEF;
     PROF_T0_FINE();
-    for (int r = threadIdx.x; r < L.mc; r += NT) L.dd[r] = L.lam[r] * recip(L.s[r]);
-    __syncthreads();
-    PROF_ACC_FINE0(24);
     assemble(P, L, L.dd, 0.0);
     PROF_ACC_FINE0(29);
-    newton_rhs_body(L, 0, 0.0);
+    newton_rhs_body<false>(L, 0, 0.0);
     PROF_ACC_FINE0(28);
     return cholesky(L) ? 1 : 0;
 }
@@ -2519,15 +2527,21 @@ __device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
     const double xw = L.dz[L.N];
     double viol = -1e300, yneg = -1e300;
     for (int r = threadIdx.x; r < L.mc; r += NT) {
-        const double rpr = gx_row(L, L.dz, xw, r) - hval(L, r);
+        const double hr = hval(L, r);
+        const double rpr = gx_row(L, L.dz, xw, r) - hr;
         L.rp[r] = rpr;
-        if (L.sa[r] != 0.0) {
-            const double y = L.la[r] + rpr * idl;
+        const double sar = L.sa[r];
+        double y = L.la[r];
+        if (sar != 0.0) {
+            y = y + rpr * idl;
             L.la[r] = y;
             yneg = fmax(yneg, -y);
         } else {
             viol = fmax(viol, rpr);
         }
+        // the next refinement's tv = mask (h / delta - y) (polish_rhs_body), formed here
+        // in the row's own thread: its pass and barrier leave the multiplier iteration
+        L.tv[r] = sar * (hr * idl - y);
     }
     double dmax = 0.0, xmax = 0.0;
     for (int e = threadIdx.x; e < L.n; e += NT) {
@@ -2545,7 +2559,7 @@ __device__ __forceinline__ D4 polish_dual_body(const cParams& P, const LT& L) {
 PHASE D4 ph_polish_dual_next(Ctx c, int ref, int cap, double early) {
     LAYDEF;
     const D4 d = polish_dual_body(P, L);
-    if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) polish_rhs_body(P, L);
+    if (polish_stop(d, ref, early) == 0 && ref + 1 < cap) rhs_from_tv_body(P, L, P.polRho);
     return d;
 }
 // certify the polished point (primal feasible, y >= 0, finite); accept -> z.
@@ -2616,12 +2630,13 @@ PHASE void ph_trace_rows(Ctx c, double* dst) {
     }
 }
 // After the evaluation: the QP's solution, its slack and the stopping-rule terms.
-PHASE void ph_trace_sol(Ctx c, double* dst, D4 ev, double delta, int ipm, int qfl, double merit0) {
+PHASE void ph_trace_sol(Ctx c, double* dst, D4 ev, double delta, int ipm, int qfl, double merit0,
+                        int rounds, int refines) {
     LAYDEF;
     for (int i = threadIdx.x; i < L.N; i += NT) dst[kTraceHdr + P.nV * P.hpMax + i] = L.ub[i];
     if (threadIdx.x == 0) {
         dst[8] = merit0;   // obj_0 + 1e5 max_violation_0 before this iteration (delta_hat, :159)
-        dst[9] = 0.0;
+        dst[9] = rounds + 4096.0 * refines;   // this QP's polish rounds and refinement solves
         dst[0] = delta;
         dst[1] = ev.a;
         dst[2] = ev.b;
@@ -2954,7 +2969,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             // warm start from the previous QP's active set from the third QP on: the
             // first re-linearisation moves the active set too far for a few
             // active-set corrections to recover it (tools/polish_study.py: 0/16)
-            const int ipm_before = qs.ipm;
+            const int ipm_before = qs.ipm, rounds_before = qs.rounds, refine_before = qs.refine;
             const bool warm_qp = warm_on && prev_ok && it >= 2;
             prev_ok = qp_solve<HG, VG, RM, OCC, SH>(c, &qflags, warm_qp, qs);
 #ifdef SCPQP_PROF
@@ -2970,7 +2985,8 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             const double delta = merit0 - (ev.obj + P.slackW * ev.maxv);
             if (trp)
                 PH(ph_trace_sol)(c, trp, D4{ev.obj, ev.maxv, ev.sumv, (double)ev.feasible}, delta,
-                                 qs.ipm - ipm_before, (prev_ok ? 1 : 0) | (warm_qp ? 2 : 0), merit0);
+                                 qs.ipm - ipm_before, (prev_ok ? 1 : 0) | (warm_qp ? 2 : 0), merit0,
+                                 qs.rounds - rounds_before, qs.refine - refine_before);
             obj0 = ev.obj;
             mv0 = ev.maxv;
             if (!isfinite(ev.obj)) {

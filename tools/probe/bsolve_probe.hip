@@ -7,6 +7,141 @@
 
 #include <vector>
 
+
+namespace {
+// Rolled blocked solve (one runtime loop per 64-row slot, BS = 4): the next block's X
+// entries and L entries are loaded one block ahead, every block's solution is captured
+// into its owner lanes with v_cndmask (no store, no branch), and a partial last block
+// is masked by zeroing its missing solution entries.
+template <int R, int BS, class HP>
+struct BSolver2 {
+    HP H;
+    const ldouble* dinv;
+    int lane, n;
+    double r[R], xf[R];
+    int ro[R], ic[R];
+    __device__ __forceinline__ BSolver2(HP H_, const ldouble* dinv_, int n_, const ldouble* bvec)
+        : H(H_), dinv(dinv_), n(n_) {
+        lane = threadIdx.x & 63;
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            const int i = lane + 64 * t;
+            ic[t] = i < n ? i : n - 1;
+            ro[t] = roff(ic[t]);
+            r[t] = i < n ? bvec[i] : 0.0;
+            xf[t] = 0.0;
+        }
+    }
+    struct Blk {
+        double x[BS * (BS - 1) / 2];
+        double l[R][BS];
+    };
+    __device__ __forceinline__ void load_x(Blk& b, int j0) {
+        int q = 0;
+#pragma unroll
+        for (int c = 1; c < BS; ++c)
+#pragma unroll
+            for (int m = 0; m < c; ++m) b.x[q++] = H[roff(j0 + c) + j0 + m];
+    }
+    template <int T0>
+    __device__ __forceinline__ void load_f(Blk& b, int j0) {
+        load_x(b, j0);
+#pragma unroll
+        for (int t = T0; t < R; ++t)
+#pragma unroll
+            for (int c = 0; c < BS; c += 2) {
+                const double2v v = ld2(H + ro[t] + j0 + c);
+                b.l[t][c] = v.x;
+                b.l[t][c + 1] = v.y;
+            }
+    }
+    template <int T1>
+    __device__ __forceinline__ void load_b(Blk& b, int j0) {
+        load_x(b, j0);
+#pragma unroll
+        for (int c = 0; c < BS; ++c) {
+            const int row = min(j0 + c, n - 1);
+#pragma unroll
+            for (int t = 0; t <= T1 && t < R; ++t) b.l[t][c] = H[roff(row) + ic[t]];
+        }
+    }
+    template <int T>
+    __device__ __forceinline__ void fwd(Blk& cur) {
+        if constexpr (T < R) {
+            const int jend = min(n, 64 * (T + 1));
+#pragma unroll 1
+            for (int j0 = 64 * T; j0 < jend; j0 += BS) {
+                Blk nxt;
+                if (j0 + BS < n) load_f<T>(nxt, j0 + BS);
+                double rb[BS], y[BS];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) rb[c] = readlane_d(r[T], (j0 + c) & 63);
+                int q = 0;
+#pragma unroll
+                for (int c = 0; c < BS; ++c) {
+                    double s = rb[c];
+#pragma unroll
+                    for (int m = 0; m < c; ++m) s = fma(cur.x[q++], rb[m], s);
+                    y[c] = j0 + c < n ? s : 0.0;
+                    xf[T] = lane == ((j0 + c) & 63) ? y[c] : xf[T];
+                }
+#pragma unroll
+                for (int t = T; t < R; ++t)
+#pragma unroll
+                    for (int c = 0; c < BS; ++c) r[t] = fma(-cur.l[t][c], y[c], r[t]);
+                cur = nxt;
+            }
+        }
+    }
+    template <int T>
+    __device__ __forceinline__ void bwd(Blk& cur, int jlast) {
+        if constexpr (T < R) {
+            const int jstart = (T == R - 1) ? jlast : 64 * T + 64 - BS;
+#pragma unroll 1
+            for (int j0 = jstart; j0 >= 64 * T; j0 -= BS) {
+                Blk nxt;
+                if (j0 > 0) load_b<T>(nxt, j0 - BS);
+                double rb[BS], y[BS];
+#pragma unroll
+                for (int c = 0; c < BS; ++c) rb[c] = readlane_d(r[T], (j0 + c) & 63);
+#pragma unroll
+                for (int c = BS - 1; c >= 0; --c) {
+                    double s = rb[c];
+#pragma unroll
+                    for (int m = BS - 1; m > c; --m) {
+                        const int q = m * (m - 1) / 2 + c;   // X[m][c]
+                        s = fma(cur.x[q], j0 + m < n ? rb[m] : 0.0, s);
+                    }
+                    y[c] = j0 + c < n ? s : 0.0;
+                    xf[T] = lane == ((j0 + c) & 63) ? y[c] : xf[T];
+                }
+#pragma unroll
+                for (int t = 0; t <= T; ++t)
+#pragma unroll
+                    for (int c = BS - 1; c >= 0; --c) r[t] = fma(-cur.l[t][c], y[c], r[t]);
+                cur = nxt;
+            }
+        }
+    }
+    __device__ __forceinline__ void run(ldouble* x) {
+        Blk cur;
+        load_f<0>(cur, 0);
+        fwd<0>(cur); fwd<1>(cur); fwd<2>(cur); fwd<3>(cur);
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+            r[t] = xf[t] * dinv[ic[t]];
+            xf[t] = 0.0;
+        }
+        const int jlast = ((n - 1) / BS) * BS;
+        load_b<R - 1>(cur, jlast);
+        bwd<3>(cur, jlast); bwd<2>(cur, jlast); bwd<1>(cur, jlast); bwd<0>(cur, jlast);
+#pragma unroll
+        for (int t = 0; t < R; ++t)
+            if (lane + 64 * t < n) x[lane + 64 * t] = xf[t];
+    }
+};
+}  // namespace
+
 namespace {
 template <int VAR, int NC>
 __global__ __launch_bounds__(256, 2) void probe(double* xout, long long* cyc, int reps) {
@@ -26,7 +161,7 @@ __global__ __launch_bounds__(256, 2) void probe(double* xout, long long* cyc, in
         b[i] = cos(0.37 * i);
     }
     __syncthreads();
-    if (VAR == 1) block_inverses<4>(H, n);
+    if (VAR == 1 || VAR == 3) block_inverses<4>(H, n);
     if (VAR == 2) block_inverses<8>(H, n);
     __syncthreads();
     if (wave_id() == 0) {
@@ -38,8 +173,11 @@ __global__ __launch_bounds__(256, 2) void probe(double* xout, long long* cyc, in
             } else if constexpr (VAR == 1) {
                 BSolver<R, 4, ldouble*> S(H, dinv, n, b);
                 S.run(x);
-            } else {
+            } else if constexpr (VAR == 2) {
                 BSolver<R, 8, ldouble*> S(H, dinv, n, b);
+                S.run(x);
+            } else {
+                BSolver2<R, 4, ldouble*> S(H, dinv, n, b);
                 S.run(x);
             }
             __builtin_amdgcn_s_waitcnt(0);
@@ -87,6 +225,7 @@ void all(double* dx, long long* dc) {
         run<0, NC>("Solver", grid, 50, dx, dc, xr.data());
         run<1, NC>("BSolver<4>", grid, 50, dx, dc, xr.data());
         run<2, NC>("BSolver<8>", grid, 50, dx, dc, xr.data());
+        run<3, NC>("BSolver2<4>", grid, 50, dx, dc, xr.data());
     }
 }
 
