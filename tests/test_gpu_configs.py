@@ -147,45 +147,55 @@ def _oracle_modes_job(args):
 # Capped problems (the SCP loop ends at the reference's 20-QP cap without meeting its
 # stopping rule, SCP_controller.py:86, 191-195).  Their iterates oscillate, so rounding
 # differences that the stopping rule forgives on a converged problem are carried through
-# all 20 iterations.  Every capped problem is compared per SCP iteration against the
-# restatement (exact-polish mode).  The tolerance, per iteration it:
-#     |u_dev(it) - u_exact(it)| <= max(CAPPED_U_TOL, U_TOL + |u_reg(it) - u_exact(it)|)
-# i.e. the converged-problem tolerance (1e-7 rad) widened by the restatement's own spread
-# between its two polish modes at that iteration (the reference's answer is not pinned
-# more tightly than that: both modes certify a KKT point of the same QP), with a floor
-# CAPPED_U_TOL = 1e-5 rad, the spread of the device's own capped c3 iterates between two
-# IPM tolerances (1e-9 vs 3e-9, DESIGN §3: up to 1.2e-5 rad).  The final u and trajectory
-# are held to CAPPED_U_TOL and CAPPED_TRAJ_TOL = 1e-4 m.
-CAPPED_U_TOL = 1e-5
-CAPPED_TRAJ_TOL = 1e-4
+# all 20 iterations.  Every capped problem is held, per SCP iteration it, to
+#     |u_dev(it) - u_reg(it)|   <= U_TOL                       (1e-7 rad)
+#     |u_dev(it) - u_exact(it)| <= U_TOL + |u_reg(it) - u_exact(it)|
+# where u_exact / u_reg are the restatement's two polish modes (the reference's exact KKT
+# polish and the device's regularised one, oracle/scp_reference.py).  The first line is
+# the converged-problem tolerance against the restatement of the device's own algorithm;
+# the second widens it only by the restatement's own mode-to-mode spread at that iteration
+# (the reference's answer is not pinned more tightly than that: both modes certify a KKT
+# point of the same QP).  No floor derived from the device's own results.  The final u and
+# trajectory are held the same way (U_TOL, TRAJ_TOL against the regularised mode; plus the
+# final mode spread against the exact one).  Measured (profiles/r05_capped.txt): the device
+# tracks the regularised restatement to <= 3e-9 rad at every iteration of every capped
+# problem; the mode spread reaches 2.1e-5 rad (c2 problem 323, QP 2).
 
 
 def _check_capped(out, b, nV, H, r_exact, r_reg, what):
     assert r_exact.n_scp == R.MAX_SCP_ITER and not r_exact.converged, what
+    assert r_reg.n_scp == R.MAX_SCP_ITER and not r_reg.converged, what
     assert int(out.n_scp[b].item()) == R.MAX_SCP_ITER, what
     tr = SP.device_trace(out, b, nV, 0, H, H)
     N = nV * H
-    e_dev = e_mode = 0.0
+    e_dev = e_reg = e_mode = 0.0
     for it in range(R.MAX_SCP_ITER):
-        ed = float(np.max(np.abs(tr[it]["z"][:N] - r_exact.history[it]["z"][:N])))
-        em = (float(np.max(np.abs(r_reg.history[it]["z"][:N] - r_exact.history[it]["z"][:N])))
-              if it < r_reg.n_scp else 0.0)
-        assert ed <= max(CAPPED_U_TOL, SP.U_TOL + em), \
-            f"{what}: iteration {it} |u| err {ed:.2e} rad, restatement mode spread {em:.2e}"
-        e_dev, e_mode = max(e_dev, ed), max(e_mode, em)
-    ub, tb = unpack_problem(out, b, nV, H)
-    e_u = float(np.max(np.abs(ub.cpu().numpy() - r_exact.u)))
-    e_t = float(np.max(np.abs(tb.cpu().numpy() - r_exact.traj)))
-    print(f"{what}: per-iteration |u| err {e_dev:.2e} rad, final |u| {e_u:.2e} rad, "
-          f"|traj| {e_t:.2e} m; restatement mode spread {e_mode:.2e} rad")
-    assert e_u <= CAPPED_U_TOL, what
-    assert e_t <= CAPPED_TRAJ_TOL, what
+        zd = tr[it]["z"][:N]
+        ed = float(np.max(np.abs(zd - r_exact.history[it]["z"][:N])))
+        er = float(np.max(np.abs(zd - r_reg.history[it]["z"][:N])))
+        em = float(np.max(np.abs(r_reg.history[it]["z"][:N] - r_exact.history[it]["z"][:N])))
+        assert er <= SP.U_TOL, \
+            f"{what}: iteration {it} |u - u_reg| {er:.2e} rad"
+        assert ed <= SP.U_TOL + em, \
+            f"{what}: iteration {it} |u - u_exact| {ed:.2e} rad, restatement mode spread {em:.2e}"
+        e_dev, e_reg, e_mode = max(e_dev, ed), max(e_reg, er), max(e_mode, em)
+    ub, tb = (t.cpu().numpy() for t in unpack_problem(out, b, nV, H))
+    e_u = float(np.max(np.abs(ub - r_exact.u)))
+    e_t = float(np.max(np.abs(tb - r_exact.traj)))
+    r_u = float(np.max(np.abs(ub - r_reg.u)))
+    r_t = float(np.max(np.abs(tb - r_reg.traj)))
+    m_u = float(np.max(np.abs(r_reg.u - r_exact.u)))
+    m_t = float(np.max(np.abs(r_reg.traj - r_exact.traj)))
+    print(f"{what}: per-iteration |u - u_exact| {e_dev:.2e} |u - u_reg| {e_reg:.2e} rad; final "
+          f"|u - u_reg| {r_u:.2e} rad |traj - traj_reg| {r_t:.2e} m; mode spread {e_mode:.2e} rad")
+    assert r_u <= SP.U_TOL and r_t <= SP.TRAJ_TOL, what
+    assert e_u <= SP.U_TOL + m_u and e_t <= SP.TRAJ_TOL + m_t, what
     return e_dev, e_mode
 
 
 def test_capped_problems_within_stated_tolerance(gpu):
     """Every capped problem of the c2 batch (B = 1024) and of the first 32 problems of the
-    c3 stream, per SCP iteration against the restatement, to CAPPED_U_TOL (above).
+    c3 stream, per SCP iteration against both restatement modes (contract above).
     Problems 14 and 18 of the c3 stream, whose two restatement modes agree to 2e-10 m over
     all 20 iterations, are held to the converged-problem tolerances (1e-7 rad)."""
     worst = {}
