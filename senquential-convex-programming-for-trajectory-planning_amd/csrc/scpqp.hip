@@ -1477,12 +1477,12 @@ typedef double double4v __attribute__((ext_vector_type(4)));
 // U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
 // budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
 // tools/gpu_ab_libs.sh.
-// part: 0 all tiles; 1 / 2 the tile columns left / right of the split that halves
-// the tile count (column tile 0, the next panels' columns, always in part 1).
+// part: 0 all tiles; 1 .. np the tile columns between the cuts that split the tile
+// count into np equal shares (column tile 0, the next panels' columns, always in part 1).
 // Tiles are enumerated column by column, so each part is a contiguous range.
 template <int U, int KS, class HP>
 __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
-                                                     int wave, int nwave, int part = 0) {
+                                                     int wave, int nwave, int part = 0, int np = 1) {
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     double dk[KS];
 #pragma unroll
@@ -1491,13 +1491,18 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
     const int ntile = T * (T + 1) / 2;
     int tb = 0, te = ntile;
     if (part != 0) {
+        // part p of np: the tile columns from the (p-1)-th to the p-th cut, the k-th cut
+        // being the first tile-column boundary with >= k ntile / np tiles before it
+        // (tile column 0 always in part 1)
         int js = 1, cum = T;   // tiles in the tile columns < js
-        while (js < T && 2 * cum < ntile) {
-            cum += T - js;
-            ++js;
+        for (int k = 1; k < np; ++k) {
+            while (js < T && np * cum < k * ntile) {
+                cum += T - js;
+                ++js;
+            }
+            if (k == part - 1) tb = cum;
+            if (k == part) te = cum;
         }
-        if (part == 1) te = cum;
-        else tb = cum;
     }
     for (int t = tb + wave; t < te; t += U * nwave) {
         double a[U][KS], b[U][KS];
@@ -1546,11 +1551,16 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
 // Grouped trailing update (factor in the global workspace): the update streams
 // the whole remaining factor through L2 once per application, and for n = 241 it
 // is the factorisation's critical path.  The trailing waves therefore apply the
-// rank-(G CB) update of G panels at once, on steps s = 0 mod G, and idle on the
-// others; the lead's look-ahead covers every panel factored since the last group
-// update.  1/G of the passes over the factor, at the price of G - 1 exposed panel
-// chains per group (G = 2: c3 3.51-3.55k -> 4.04-4.07k solves/s).
-constexpr int kGroup = 2;   // panels per grouped trailing update (4 measured slower)
+// rank-(G CB) update of G panels at once, spread over the next group's G steps
+// (trailing_update_mfma parts); the lead's look-ahead covers every panel factored
+// since the last group update.  1/G of the passes over the factor (G = 2: c3
+// 3.51-3.55k -> 4.04-4.07k solves/s).
+// panels per grouped trailing update: 4 since round 5 (c3 +1-2 % against 2 in one session,
+// HBM traffic 2.93 -> 2.35 TB per launch; unsplit in round 2 it measured slower)
+#ifndef SCPQP_GROUP
+#define SCPQP_GROUP 4
+#endif
+constexpr int kGroup = SCPQP_GROUP;
 static_assert(2 * kGroup * CB <= 64, "the pivot buffer holds 64 entries");
 
 template <class LT>
@@ -1580,22 +1590,18 @@ __device__ bool cholesky(const LT& L) {
             if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             lead_prio_down();
-        } else if ((jp >= 0 || (G == 2 && s >= 3)) && r0 < n) {
+        } else if (jp >= 0 || (G > 1 && s >= G)) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL) {
                 constexpr int U = LT::OCCV >= 3 ? 2 : 4;   // tiles in flight per wave
-                if constexpr (G == 2) {
-                    // the pair's update in two halves: the left tile columns (they hold
-                    // the next two panels) on the even step, the rest on the odd step,
-                    // so the odd step's panel chain runs beside the trailing update
-                    if (sg == 0)
-                        trailing_update_mfma<U, 2 * CB / 4>(L.H, n, jp, r1, dprev, tw, NWAVE - 1, 1);
-                    else if (s >= 3)
-                        trailing_update_mfma<U, 2 * CB / 4>(L.H, n, r0 - 3 * CB, r0, dbuf + ((s - 3) & 3) * CB,
-                                                            tw, NWAVE - 1, 2);
-                } else if (sg == 0) {
-                    trailing_update_mfma<U, G * CB / 4>(L.H, n, jp, r1, dprev, tw, NWAVE - 1);
-                }
+                // the previous group's update in G parts, part sg + 1 on step sg of this
+                // group: the left tile columns (they hold the next panels) on its first
+                // step, so every later step's panel chain runs beside a share of the update
+                const int s0 = s - sg;   // this group's first step
+                if (s0 >= G)
+                    trailing_update_mfma<U, G * CB / 4>(L.H, n, (s0 - G) * CB, s0 * CB + CB,
+                                                        dbuf + ((s0 - G) & (2 * G - 1)) * CB,
+                                                        tw, NWAVE - 1, sg + 1, G);
             } else {
                 trailing_update(L.H, n, jp, r1, dprev, tw * 64 + (int)(threadIdx.x & 63), NT - 64);
 #ifdef SCPQP_DIAG_X2_TRAIL   // counter attribution: a result-neutral second pass
