@@ -45,8 +45,8 @@ FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD da
 HBM_PEAK_GBS = 8000.0
 METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
 # committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu.sh pmc + pmc_summary.py)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04_pmc_traffic_{}.json")
-PMC_SQ = os.path.join(ROOT, "profiles", "r04_pmc_sq_{}.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic_{}.json")
+PMC_SQ = os.path.join(ROOT, "profiles", "r05_pmc_sq_{}.json")
 
 
 # ----------------------------------------------------------------------------- CPU baseline
