@@ -1014,32 +1014,15 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
             wm0 = ld2(W + 4 * k1 * nb);
             wm1 = ld2(W + 4 * k1 * nb + 2);
         }
-        for (int k = k0; k < Hb; ++k) {
+        auto trip = [&](const double2v& anew, const double2v& bnew, const double2v& w0,
+                        const double2v& w1) {
 #pragma unroll
             for (int i = TS - 1; i > 0; --i) {
                 av[i] = av[i - 1];
                 bv[i] = bv[i - 1];
             }
-            av[0] = an;
-            bv[0] = bn;
-            const double2v w0 = wn0, w1 = wn1;
-            if constexpr (PF2) {
-                an = an2;
-                bn = bn2;
-                wn0 = wm0;
-                wn1 = wm1;
-                const int kn = k + 2 < Hb ? k + 2 : Hb - 1;
-                an2 = ld2(ga + 2 * (kn - l0));
-                bn2 = ld2(gb + 2 * (kn - m0));
-                wm0 = ld2(W + 4 * kn * nb);
-                wm1 = ld2(W + 4 * kn * nb + 2);
-            } else {
-                const int kn = k + 1 < Hb ? k + 1 : k;   // the last step reloads its own
-                an = ld2(ga + 2 * (kn - l0));
-                bn = ld2(gb + 2 * (kn - m0));
-                wn0 = ld2(W + 4 * kn * nb);
-                wn1 = ld2(W + 4 * kn * nb + 2);
-            }
+            av[0] = anew;
+            bv[0] = bnew;
             double px[TS], py[TS];   // W~ g_b for every column
 #pragma unroll
             for (int j = 0; j < TS; ++j) {
@@ -1052,6 +1035,47 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
             for (int i = 0; i < TS; ++i)
 #pragma unroll
                 for (int j = 0; j < TS; ++j) c[i][j] = fma(av[i].y, py[j], fma(av[i].x, px[j], c[i][j]));
+        };
+        if constexpr (!PF2) {
+            // LDS factors, ping-pong (round 5): two operand sets, each loaded one trip
+            // ahead of its use and held ahead of the other trip's arithmetic
+            // (sched_barrier), with no loop-carried register rotation, which made the
+            // compiler wait for the load it had just issued (B = 1: 67.9k -> 64.9k cycles
+            // per IPM iteration for assembly + factorisation, c2 +1.3 %)
+            double2v a1 = an, b1 = bn, w10 = wn0, w11 = wn1;
+            int k = k0;
+#pragma unroll 1
+            for (; k + 1 < Hb; k += 2) {
+                a1 = ld2(ga + 2 * (k + 1 - l0));
+                b1 = ld2(gb + 2 * (k + 1 - m0));
+                w10 = ld2(W + 4 * (k + 1) * nb);
+                w11 = ld2(W + 4 * (k + 1) * nb + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                trip(an, bn, wn0, wn1);
+                const int kn = k + 2 < Hb ? k + 2 : Hb - 1;
+                an = ld2(ga + 2 * (kn - l0));
+                bn = ld2(gb + 2 * (kn - m0));
+                wn0 = ld2(W + 4 * kn * nb);
+                wn1 = ld2(W + 4 * kn * nb + 2);
+                __builtin_amdgcn_sched_barrier(0);
+                trip(a1, b1, w10, w11);
+            }
+            if (k < Hb) trip(an, bn, wn0, wn1);
+            (void)an2; (void)bn2; (void)wm0; (void)wm1;
+        } else {
+            for (int k = k0; k < Hb; ++k) {
+                const double2v acur = an, bcur = bn, w0 = wn0, w1 = wn1;
+                an = an2;
+                bn = bn2;
+                wn0 = wm0;
+                wn1 = wm1;
+                const int kn = k + 2 < Hb ? k + 2 : Hb - 1;
+                an2 = ld2(ga + 2 * (kn - l0));
+                bn2 = ld2(gb + 2 * (kn - m0));
+                wm0 = ld2(W + 4 * kn * nb);
+                wm1 = ld2(W + 4 * kn * nb + 2);
+                trip(acur, bcur, w0, w1);
+            }
         }
 #pragma unroll
         for (int di = 0; di < TS; ++di)
@@ -1693,6 +1717,12 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
 #pragma unroll
             for (int q = 0; q < SCH; ++q) cur[t][q] = nxt[t][q];
     }
+    // the solution entry j (uniform xj) into its owner lane (v_writelane through M0 is
+    // bitwise the same but kept the sweep from unrolling: solves 21.2k -> 31.3k cycles per
+    // IPM iteration at B = 1, c2 -7 %, profiles/r05_ab_writelane.txt)
+    __device__ __forceinline__ double capture(double xj, int j, double old) const {
+        return (lane == (j & 63)) ? xj : old;
+    }
     // forward over the columns owned by slot T (compile-time owner); slots < T are final
     template <int T>
     __device__ __forceinline__ void fwd() {
@@ -1706,7 +1736,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
                     if (j < jend) {
                         const double xj = readlane_d(r[T], j & 63);
                         r[T] -= cur[T][q] * xj;
-                        xf[T] = (lane == (j & 63)) ? xj : xf[T];
+                        xf[T] = capture(xj, j, xf[T]);
 #pragma unroll
                         for (int t = T + 1; t < R; ++t) r[t] -= cur[t][q] * xj;
                     }
@@ -1729,7 +1759,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
                         const double xj = readlane_d(r[T], j & 63);
                         // the owner slot first: it carries the next step's broadcast
                         r[T] -= cur[T][q] * xj;
-                        xf[T] = (lane == (j & 63)) ? xj : xf[T];
+                        xf[T] = capture(xj, j, xf[T]);
 #pragma unroll
                         for (int t = 0; t < T; ++t) r[t] -= cur[t][q] * xj;
                     }
