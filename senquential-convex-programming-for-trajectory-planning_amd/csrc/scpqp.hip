@@ -260,14 +260,20 @@ struct Lay {
 // index division and LDS offset built from them folds at compile time (vehicle
 // loops unrolled, Toeplitz trip counts known).  0 = runtime shape (any problem);
 // a fixed horizon is used only when every problem of the launch has hp = hp_max.
+// H: the problem's horizon; HM: the slot horizon the layout is planned for (hp_max).
+// Shapes 4-6 are c5's horizon classes: the mixed-horizon kernel (shape 2) runs each
+// problem's QPs with its horizon compiled in, in the launch's hp_max layout (round 5).
 struct ShapeC {
-    int V, O, H;
+    int V, O, H, HM;
 };
 __host__ __device__ constexpr ShapeC shape_c(int sh) {
-    return sh == 1 ? ShapeC{4, 0, 20}     // c2 / c4: 4 vehicles, Hp 20
-         : sh == 2 ? ShapeC{4, 0, 0}      // c5: 4 vehicles, mixed horizons
-         : sh == 3 ? ShapeC{8, 0, 30}     // c3: 8 vehicles, Hp 30
-                   : ShapeC{0, 0, 0};
+    return sh == 1 ? ShapeC{4, 0, 20, 20}     // c2 / c4: 4 vehicles, Hp 20
+         : sh == 2 ? ShapeC{4, 0, 0, 0}       // c5: 4 vehicles, mixed horizons
+         : sh == 3 ? ShapeC{8, 0, 30, 30}     // c3: 8 vehicles, Hp 30
+         : sh == 4 ? ShapeC{4, 0, 10, 0}      // c5 classes (QP solves of shape 2)
+         : sh == 5 ? ShapeC{4, 0, 20, 0}
+         : sh == 6 ? ShapeC{4, 0, 30, 0}
+                   : ShapeC{0, 0, 0, 0};
 }
 template <int SH>
 __host__ __device__ __forceinline__ int shapeV(int v) { return shape_c(SH).V ? shape_c(SH).V : v; }
@@ -275,6 +281,8 @@ template <int SH>
 __host__ __device__ __forceinline__ int shapeO(int o) { return shape_c(SH).V ? shape_c(SH).O : o; }
 template <int SH>
 __host__ __device__ __forceinline__ int shapeH(int h) { return shape_c(SH).H ? shape_c(SH).H : h; }
+template <int SH>
+__host__ __device__ __forceinline__ int shapeHM(int h) { return shape_c(SH).HM ? shape_c(SH).HM : h; }
 
 template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* ws, const Off& f, int V,
@@ -815,7 +823,7 @@ __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int 
     Hb = __builtin_amdgcn_readfirstlane(Hb);
     const cKArgs& a = *ap;
     const cParams& P = *(const cParams*)a.P;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
     const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
 }
@@ -1666,8 +1674,9 @@ __device__ bool cholesky(const LT& L) {
 
 constexpr int kSolveChunk = 4;    // chunk of a factor in LDS
 constexpr int kSolveChunkG = 8;   // chunk of a factor in the workspace: twice the steps cover the L2 latency
-template <int R, class HP, int SCH>
-struct Solver {   // SCH: chunk (columns / rows) streamed per step group
+template <int R, class HP, int SCH, bool RTN = false>
+struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n not a
+                  // compile-time constant (the chunk loops stay rolled, below)
     static_assert(SCH % 2 == 0 && 64 % SCH == 0, "chunks tile the 64-row slots");
     HP H;                   // factor (LDS or workspace)
     const ldouble* dinv;
@@ -1728,7 +1737,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
     __device__ __forceinline__ void fwd() {
         if constexpr (T < R) {
             const int jend = min(n, 64 * (T + 1));
-            for (int jc = 64 * T; jc < jend; jc += SCH) {
+            auto chunk = [&](int jc) {
                 if (jc + SCH < n) load_cols(nxt, jc + SCH);
 #pragma unroll
                 for (int q = 0; q < SCH; ++q) {
@@ -1742,6 +1751,15 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
                     }
                 }
                 shift();
+            };
+            if constexpr (RTN) {
+                // with a run-time n the compiler unrolled this loop once per possible
+                // remainder (248 VGPRs, stack reloads inside the sweep: c5's mixed
+                // horizons); rolled it stays one chunk body
+#pragma unroll 1
+                for (int jc = 64 * T; jc < jend; jc += SCH) chunk(jc);
+            } else {
+                for (int jc = 64 * T; jc < jend; jc += SCH) chunk(jc);
             }
         }
     }
@@ -1750,7 +1768,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
     __device__ __forceinline__ void bwd(int jlast) {
         if constexpr (T < R) {
             const int jstart = (T == R - 1) ? jlast : 64 * T + 64 - SCH;
-            for (int jc = jstart; jc >= 64 * T; jc -= SCH) {
+            auto chunk = [&](int jc) {
                 if (jc > 0) load_rows(nxt, jc - SCH);
 #pragma unroll
                 for (int q = SCH - 1; q >= 0; --q) {
@@ -1765,6 +1783,12 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
                     }
                 }
                 shift();
+            };
+            if constexpr (RTN) {
+#pragma unroll 1
+                for (int jc = jstart; jc >= 64 * T; jc -= SCH) chunk(jc);
+            } else {
+                for (int jc = jstart; jc >= 64 * T; jc -= SCH) chunk(jc);
             }
         }
     }
@@ -1791,14 +1815,19 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group
     }
 };
 
-template <int R, class LT>
+template <int R, bool RTN, class LT>
 __device__ __forceinline__ void chol_solve_r(const LT& L, const ldouble* bvec, ldouble* x) {
-    Solver<R, decltype(L.H), (LT::HGLOBAL ? kSolveChunkG : kSolveChunk)> S(L.H, L.dinv, L.n, L.ld, bvec);
+    Solver<R, decltype(L.H), (LT::HGLOBAL ? kSolveChunkG : kSolveChunk), RTN> S(L.H, L.dinv, L.n, L.ld, bvec);
     S.run(x);
 }
 
-template <class LT>
+// SH: the problem shape.  A run-time horizon (shapes 0 and 2) keeps the sweeps' chunk
+// loops rolled; c5's horizon classes run as shapes 4-6 with n compiled in (the kernel's
+// QP dispatch), unrolled like c2's (c5 B = 1 Hp 30: solves 62.3k -> 33.2k cycles per IPM
+// iteration, c5 117.7k -> 135k solves/s, profiles/r05_ab_c5_solve_classes.txt).
+template <int SH, class LT>
 __device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
+    constexpr bool RTN = shape_c(SH).H == 0;
 #ifdef SCPQP_DIAG_X2_SOLVE   // counter attribution: the solve twice (the same x)
     for (int rep = 0; rep < 2; ++rep)
 #endif
@@ -1806,10 +1835,10 @@ __device__ void chol_solve(const LT& L, const ldouble* bvec, ldouble* x) {
         const int n = L.n;
         constexpr int RM = LT::RMAX;
         lead_prio_up();
-        if (RM == 1 || n <= 64) chol_solve_r<1>(L, bvec, x);
-        else if (RM == 2 || n <= 128) chol_solve_r<(RM >= 2 ? 2 : 1)>(L, bvec, x);
-        else if (RM == 3 || n <= 192) chol_solve_r<(RM >= 3 ? 3 : 1)>(L, bvec, x);
-        else chol_solve_r<RM>(L, bvec, x);
+        if (RM == 1 || n <= 64) chol_solve_r<1, RTN>(L, bvec, x);
+        else if (RM == 2 || n <= 128) chol_solve_r<(RM >= 2 ? 2 : 1), RTN>(L, bvec, x);
+        else if (RM == 3 || n <= 192) chol_solve_r<(RM >= 3 ? 3 : 1), RTN>(L, bvec, x);
+        else chol_solve_r<RM, RTN>(L, bvec, x);
         lead_prio_down();
     }
     __syncthreads();
@@ -2060,7 +2089,7 @@ __device__ __forceinline__ Ctx uniform_ctx(const Ctx& c) {
 
 template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
-    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeH<SH>(c.P->hpMax), HG, VG, !HG && VG && OCC == 2);
+    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeHM<SH>(c.P->hpMax), HG, VG, !HG && VG && OCC == 2);
     Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
     L.lead = c.lead;
     return L;
@@ -2076,7 +2105,7 @@ __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
 // x = K^{-1} rhs into z (dst = 0) or dz (dst = 1)
 PHASE void ph_solve(Ctx c, int dst) {
     LAYDEF;
-    chol_solve(L, L.rhs, dst ? L.dz : L.z);
+    chol_solve<SH>(L, L.rhs, dst ? L.dz : L.z);
 }
 PHASE void ph_linearise(Ctx c) {
     LAYDEF;
@@ -2689,7 +2718,7 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     const cParams& P = *(const cParams*)a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeH<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
     lint* slot = (lint*)(smem + f.red + 124);
     ldouble* lub = smem + f.ub;   // u-bar
     ldouble* lpb = smem + f.pb;   // positions of the last evaluated u
@@ -2802,7 +2831,14 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
             // active-set corrections to recover it (tools/polish_study.py: 0/16)
             const int ipm_before = qs.ipm, rounds_before = qs.rounds, refine_before = qs.refine;
             const bool warm_qp = warm_on && prev_ok && it >= 2;
-            prev_ok = qp_solve<HG, VG, RM, OCC, SH>(c, &qflags, warm_qp, qs);
+            if constexpr (SH == 2) {   // c5: the QP with its horizon class compiled in
+                if (Hb == 30) prev_ok = qp_solve<HG, VG, RM, OCC, 6>(c, &qflags, warm_qp, qs);
+                else if (Hb == 20) prev_ok = qp_solve<HG, VG, RM, OCC, 5>(c, &qflags, warm_qp, qs);
+                else if (Hb == 10) prev_ok = qp_solve<HG, VG, RM, OCC, 4>(c, &qflags, warm_qp, qs);
+                else prev_ok = qp_solve<HG, VG, RM, OCC, SH>(c, &qflags, warm_qp, qs);
+            } else {
+                prev_ok = qp_solve<HG, VG, RM, OCC, SH>(c, &qflags, warm_qp, qs);
+            }
 #ifdef SCPQP_PROF
             _pt = __builtin_amdgcn_s_memtime();
 #endif
