@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
             // ahead of its use and held ahead of the other trip's arithmetic
             // (sched_barrier), with no loop-carried register rotation, which made the
             // compiler wait for the load it had just issued (B = 1: 67.9k -> 64.9k cycles
-            // per IPM iteration for assembly + factorisation, c2 +1.3 %)
+            // per IPM iteration for assembly + factorisation; throughput within noise)
             double2v a1 = an, b1 = bn, w10 = wn0, w11 = wn1;
             int k = k0;
 #pragma unroll 1
