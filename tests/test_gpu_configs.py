@@ -10,6 +10,9 @@
   B = 3072 in hp_max = 30 slots (the divergent-wavefront stress configuration, per
   problem early exit, SCP_controller.py:191-195); the properties on every problem
   and per-iteration oracle parity on 12 problems of each horizon class.
+* Horizons outside c5's compiled classes (Hp 15, 25 beside Hp 30) in one launch: the
+  run-time-horizon path against the restatement, and the class path's independence
+  from its neighbours.
 """
 import multiprocessing as mp
 
@@ -122,6 +125,38 @@ def test_c5_mixed_horizon_full_batch_3072(gpu):
         ub, tb = unpack_problem(out, b, 4, H)
         SP.compare(ub.cpu().numpy(), tb.cpu().numpy(), int(out.n_scp[b].item()),
                    SP.device_trace(out, b, 4, 0, H, 30), r, 4, H, what=f"c5 problem {b} (Hp {H})")
+    S.close()
+
+
+def test_mixed_horizons_outside_the_compiled_classes(gpu):
+    """c5's kernel runs Hp 10 / 20 / 30 with the horizon compiled in (shapes 4-6, round 5)
+    and any other horizon on the run-time path of the same launch.  A launch mixing
+    Hp 30 (compiled class) with Hp 15 and 25 (run-time path): every problem matches the
+    restatement per SCP iteration, and the Hp-30 problems' results equal those of the
+    same problems in an all-Hp-30 launch of the same handle (the class path does not
+    depend on its neighbours)."""
+    sc = R.circle_scenario(4, Hp=30)
+    B, Hs = 48, (15, 25, 30)
+    bt = shard.shard_batch(sc, B, 0, base_seed=0, mixed_hp=Hs)
+    assert sorted(set(bt.hp.tolist())) == list(Hs)
+    S = ScpQpSolver(sc, max_batch=B, hp_max=30)
+    out = S.solve(bt.x0, bt.u0, bt.ec_noise, hp=bt.hp, trace=True)
+    torch.cuda.synchronize()
+    _properties(S, sc, bt, out, 4, 30, hp=bt.hp)
+    idx = [b for H in Hs for b in np.flatnonzero(bt.hp == H)[:4].tolist()]
+    jobs = [(4, int(bt.hp[b]), bt.x0[b], bt.u0[b], bt.ec_noise[b], 30) for b in idx]
+    with mp.get_context("spawn").Pool(12) as pool:
+        res = pool.map(_oracle_job, jobs)
+    for b, r in zip(idx, res):
+        H = int(bt.hp[b])
+        ub, tb = unpack_problem(out, b, 4, H)
+        SP.compare(ub.cpu().numpy(), tb.cpu().numpy(), int(out.n_scp[b].item()),
+                   SP.device_trace(out, b, 4, 0, H, 30), r, 4, H, what=f"problem {b} (Hp {H})")
+    hp30 = np.full(B, 30, dtype=bt.hp.dtype)
+    o30 = S.solve(bt.x0, bt.u0, bt.ec_noise, hp=hp30)
+    torch.cuda.synchronize()
+    sel = torch.as_tensor(np.flatnonzero(bt.hp == 30), device=out.u.device)
+    assert torch.equal(out.u.reshape(B, -1)[sel], o30.u.reshape(B, -1)[sel])
     S.close()
 
 
