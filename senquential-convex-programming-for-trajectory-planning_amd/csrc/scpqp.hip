@@ -1510,9 +1510,8 @@ __device__ __forceinline__ void trailing_update(HP H, int n, int j0, int r1, con
 // written (packed rows end at the diagonal).
 typedef double double4v __attribute__((ext_vector_type(4)));
 
-// U tiles are in flight per wave so that their L2 loads overlap: 4 at a 256-VGPR
-// budget (c3 2.37k -> 2.73k solves/s), 2 at 168 VGPRs (c5 -3.5 % at 4, more spill),
-// tools/gpu_ab_libs.sh.
+// U tiles are in flight per wave so that their L2 loads overlap (round 2, two panels per
+// update: 4 at a 256-VGPR budget, c3 2.37k -> 2.73k solves/s; round 5, four panels: 2).
 // part: 0 all tiles; 1 .. np the tile columns between the cuts that split the tile
 // count into np equal shares (column tile 0, the next panels' columns, always in part 1).
 // Tiles are enumerated column by column, so each part is a contiguous range.
@@ -1629,7 +1628,10 @@ __device__ bool cholesky(const LT& L) {
         } else if (jp >= 0 || (G > 1 && s >= G)) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
             if constexpr (LT::HGLOBAL) {
-                constexpr int U = LT::OCCV >= 3 ? 2 : 4;   // tiles in flight per wave
+                // tiles in flight per wave: 2 (round 5, with the group of four's eight MFMAs
+                // per tile: c3 5.92-6.07k -> 6.39-6.44k against 4, 1 within noise of 2;
+                // profiles/r05_ab_mfma_tiles.txt)
+                constexpr int U = 2;
                 // the previous group's update in G parts, part sg + 1 on step sg of this
                 // group: the left tile columns (they hold the next panels) on its first
                 // step, so every later step's panel chain runs beside a share of the update
