@@ -236,7 +236,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1024, help="problems per GPU (config c2: 1024)")
     ap.add_argument("--n-veh", type=int, default=4)
     ap.add_argument("--hp", type=int, default=20)
@@ -246,6 +246,8 @@ def main():
                     help="BASELINE config: c2 4 veh Hp 20 B 1024 (the metric's workload, default); "
                          "c3 8 veh Hp 30 B 4096; c4 4 veh Hp 20, 65536 problems as 8192 per "
                          "rank (8 GPUs); c5 4 veh mixed Hp {10,20,30} B 3072")
+    ap.add_argument("--lib", default=None,
+                    help="tools only: another build of the library (A/B runs, tools/gpu.sh ab)")
     args = ap.parse_args()
     mixed = None
     if args.config == "c4":
@@ -313,6 +315,9 @@ def main():
         dist = None
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.lib:
+        from scpqp import _lib
+        _lib.use_build(args.lib)
     from scpqp.solver import ScpQpSolver
 
     S = ScpQpSolver(sc, max_batch=B, device=dev)
@@ -332,19 +337,23 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
+    # one event per step boundary on the launch stream (no extra synchronisation in the
+    # timed region): the mean over the K steps prices the roofline, the median is the
+    # per-step statistic of SURVEY 8(d)
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
+    evs[0].record(stream)
+    for k in range(args.steps):
         S.solve(x0, u0, ec, hp=hpt, out=out)
-    ev1.record(stream)
+        evs[k + 1].record(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / max(args.steps, 1)   # one launch per step
+    step_ms = [evs[k].elapsed_time(evs[k + 1]) for k in range(args.steps)]
+    kern_ms = evs[0].elapsed_time(evs[-1]) / max(args.steps, 1)   # one launch per step
+    kern_ms_median = float(np.median(step_ms)) if step_ms else kern_ms
     elapsed = shard.max_over_ranks(elapsed, dist, dev)
 
     # end-to-end leg: host (pinned) inputs -> H2D -> solve -> D2H of the result
@@ -412,6 +421,10 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
+        "ms_per_step_median": shard.max_over_ranks(kern_ms_median * 1e-3, dist, dev) * 1e3,
+        "ms_per_step_note": "ms_per_step: the K timed steps' wall time / K (max over ranks); "
+                            "ms_per_step_median: median of the per-step HIP-event times on the "
+                            "launch stream (max over ranks)",
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -454,7 +467,10 @@ def main():
                      "peak_note": "FP64 dense peak (vector = MFMA rate on gfx950, AMD spec)"},
         "qp_solves_per_s": world * float(n_scp.sum()) * args.steps / elapsed,
         "mean_scp_iters": float(n_scp.mean()),
+        "max_scp_iters": int(n_scp.max()),
         "mean_ipm_iters_per_qp": float(n_ipm.sum() / max(n_scp.sum(), 1)),
+        "mean_ipm_iters_per_problem": float(n_ipm.mean()),
+        "max_ipm_iters_per_problem": int(n_ipm.max()),
         "warm_certified_qp_frac": float(n_warm.sum() / max(n_scp.sum(), 1)),
         "mean_polish_solves_per_qp": float(n_ref.sum() / max(n_scp.sum(), 1)),
         "status_converged_frac": float(np.mean((status & 0xff) == 0)),

@@ -702,7 +702,10 @@ class QPResult:
     iters: int
     converged: bool
     polished: bool
-    certificate: dict = None
+    certificate: dict = None          # unscaled KKT residuals (kkt_residuals)
+    certified: bool = False           # certificate_scaled within the CERT_* bounds
+    certificate_scaled: dict = None
+    escalations: int = 0              # fallback stages qp_solve needed (0: the first polish)
 
 
 def qp_matrices(Phi0, Psi0, A, b, u_lim):
@@ -831,6 +834,7 @@ def qp_ipm(P, q, G, h, tol=IPM_TOL, maxit=60, init="cvxopt"):
 
 
 POLISH_ROUNDS = 6           # active-set corrections of the polish (primal-dual active set)
+POLISH_SINGLE = 80          # single-row corrections of the exact polish's safeguard (below)
 
 
 def _pdas_update(G, h, act, xp, lam_act, tol=1e-9):
@@ -852,31 +856,62 @@ def _pdas_update(G, h, act, xp, lam_act, tol=1e-9):
     return False, (act & ~neg) | viol
 
 
-def qp_polish_exact(P, q, G, h, x, s, lam, rounds=POLISH_ROUNDS):
-    """Solve [P G_A'; G_A 0][x; y] = [-q; h_A] on the active set A = {lam > s},
-    correcting A until the point certifies (primal feasible, y >= 0)."""
-    act = lam > s
+def _kkt_active(P, q, G, h, act):
+    """[P G_A'; G_A 0][x; y] = [-q; h_A] (least squares if the active rows are dependent)."""
     n = len(q)
-    for _ in range(rounds):
-        Ga, ha = G[act], h[act]
-        na = int(act.sum())
-        K = np.zeros((n + na, n + na))
-        K[:n, :n] = P; K[:n, n:] = Ga.T; K[n:, :n] = Ga
-        rhs = np.concatenate([-q, ha])
-        try:
-            sol = np.linalg.solve(K, rhs)
-        except np.linalg.LinAlgError:
-            sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
-        if not np.all(np.isfinite(sol)):
+    Ga, ha = G[act], h[act]
+    na = int(act.sum())
+    K = np.zeros((n + na, n + na))
+    K[:n, :n] = P; K[:n, n:] = Ga.T; K[n:, :n] = Ga
+    rhs = np.concatenate([-q, ha])
+    try:
+        sol = np.linalg.solve(K, rhs)
+    except np.linalg.LinAlgError:
+        sol = np.linalg.lstsq(K, rhs, rcond=None)[0]
+    return sol[:n], sol[n:]
+
+
+def qp_polish_exact(P, q, G, h, x, s, lam, rounds=POLISH_ROUNDS, single=POLISH_SINGLE):
+    """Solve [P G_A'; G_A 0][x; y] = [-q; h_A] on the active set A = {lam > s},
+    correcting A until the point certifies (primal feasible, y >= 0).
+
+    Full-swap corrections first (_pdas_update).  A plain primal-dual active-set
+    iteration is not globally convergent: from a poor guess it can cycle or diverge
+    (c2 problem 323, QP 1: the coneqp-start IPM broke down with one row wrongly
+    active, and the swaps grew the infeasible set 14 -> 8 -> 148 rows; verdict r05).
+    Safeguard: once a swap would change no fewer rows than the best state so far, go
+    back to that state and correct one row at a time, the most negative multiplier
+    first, else the most violated row."""
+    act = lam > s
+    hn = max(1.0, np.abs(h).max())
+    best_n, best_act = None, act
+    one_row = False
+    for k in range(rounds + single):
+        xp, la = _kkt_active(P, q, G, h, act)
+        if not (np.all(np.isfinite(xp)) and np.all(np.isfinite(la))):
             return None
-        xp, la = sol[:n], sol[n:]
         ok, nxt = _pdas_update(G, h, act, xp, la)
         if ok:
             lam_full = np.zeros_like(lam); lam_full[act] = la
             return xp, lam_full
-        if np.array_equal(nxt, act):
-            return None
-        act = nxt
+        n_bad = int((nxt != act).sum())
+        if not one_row:
+            if best_n is not None and (n_bad >= best_n or k >= rounds):
+                one_row = True
+                act = best_act
+                continue
+            if best_n is None or n_bad < best_n:
+                best_n, best_act = n_bad, act
+            act = nxt
+            continue
+        lam_full = np.zeros(len(h)); lam_full[act] = la
+        act = act.copy()
+        if (act & (lam_full < 0)).any() and lam_full[act].min() < -1e-9 * max(1.0, np.abs(la).max()):
+            act[np.flatnonzero(act)[np.argmin(lam_full[act])]] = False
+        else:
+            r = G @ xp - h
+            r[act] = -np.inf
+            act[int(np.argmax(r))] = True
     return None
 
 
@@ -935,16 +970,70 @@ def kkt_residuals(P, q, G, h, x, lam):
                 complementarity=float(np.abs(lam * r).max()))
 
 
-def qp_solve(P, q, G, h, u_lim, N, polish="exact", tol=IPM_TOL):
-    """Scaled IPM + polish.  ``polish``: 'exact' (oracle), 'regularised' (HIP mirror), None."""
+# The oracle's acceptance bounds, on the scaled QP (controls in units of uLim, every
+# row of unit norm; qp_scale): stationarity absolute (the slack weight 1e5 sits in q,
+# so 1e-7 is 1e-12 of the largest gradient entry), primal feasibility relative to
+# max(1, |h|), dual feasibility and complementarity relative to max(1, |lam|).
+CERT_STATIONARITY = 1e-7
+CERT_PRIMAL = 1e-9
+CERT_DUAL = 1e-9
+CERT_COMPLEMENTARITY = 1e-9
+
+
+class UncertifiedQP(RuntimeError):
+    """The oracle could not certify a QP's KKT point (qp_solve raises it rather than
+    hand an uncertified answer to a parity check)."""
+
+
+def certificate_scaled(Ps, qs, Gs, hs, x, lam):
+    r = Gs @ x - hs
+    lm = max(1.0, float(np.abs(lam).max()))
+    c = dict(stationarity=float(np.abs(Ps @ x + qs + Gs.T @ lam).max()),
+             primal=float(max(r.max(), 0.0)) / max(1.0, float(np.abs(hs).max())),
+             dual=float(max(-lam.min(), 0.0)) / lm,
+             complementarity=float(np.abs(lam * r).max()) / lm)
+    c["certified"] = bool(c["stationarity"] <= CERT_STATIONARITY and c["primal"] <= CERT_PRIMAL
+                          and c["dual"] <= CERT_DUAL
+                          and c["complementarity"] <= CERT_COMPLEMENTARITY)
+    return c
+
+
+def qp_solve(P, q, G, h, u_lim, N, polish="exact", tol=IPM_TOL, require_certificate=None):
+    """Scaled IPM + polish.  ``polish``: 'exact' (oracle), 'regularised' (HIP mirror), None.
+
+    'exact' escalates until the point certifies (certificate_scaled): the coneqp-start
+    IPM and the exact KKT polish; the same IPM 100x tighter; the kernel's starting point
+    (ipm_start_omega) at both tolerances; the regularised polish from each of these
+    points.  If none certifies it raises UncertifiedQP (``require_certificate``, default
+    on for 'exact'): the parity checker never accepts an uncertified QP (verdict r05).
+    'regularised' mirrors the device, including its resumed IPM, and records whether it
+    certified (the device can end a QP uncertified too: SCPQP_FL_POLISH_REJECTED)."""
     Ps, qs, Gs, hs, sv, rn = qp_scale(P, q, G, h, u_lim, N)
+    if require_certificate is None:
+        require_certificate = polish == "exact"
     x, s, lam, it, st = qp_ipm(Ps, qs, Gs, hs, tol=tol,
                                init="omega" if polish == "regularised" else "cvxopt")
     pol = None
+    escalation = 0
     if polish == "exact":
         pol = qp_polish_exact(Ps, qs, Gs, hs, x, s, lam)
-        if pol is None:
-            pol = qp_polish_regularised(Ps, qs, Gs, hs, x, s, lam, nref=40)
+        starts = [("cvxopt", 0.01 * tol), ("omega", tol), ("omega", 0.01 * tol)]
+        for init, t in starts:
+            if pol is not None and certificate_scaled(Ps, qs, Gs, hs, *pol)["certified"]:
+                break
+            escalation += 1
+            x2, s2, lam2, it2, st2 = qp_ipm(Ps, qs, Gs, hs, tol=t, init=init)
+            pol = qp_polish_exact(Ps, qs, Gs, hs, x2, s2, lam2)
+            if pol is not None:
+                x, s, lam, it, st = x2, s2, lam2, it2, st2
+        if pol is None or not certificate_scaled(Ps, qs, Gs, hs, *pol)["certified"]:
+            for init, t in [("cvxopt", tol)] + starts:
+                escalation += 1
+                x2, s2, lam2, it2, st2 = qp_ipm(Ps, qs, Gs, hs, tol=t, init=init)
+                pol = qp_polish_regularised(Ps, qs, Gs, hs, x2, s2, lam2, nref=200)
+                if pol is not None and certificate_scaled(Ps, qs, Gs, hs, *pol)["certified"]:
+                    x, s, lam, it, st = x2, s2, lam2, it2, st2
+                    break
     elif polish == "regularised":
         pol = qp_polish_regularised(Ps, qs, Gs, hs, x, s, lam)
         if pol is None and st == 1:
@@ -955,10 +1044,14 @@ def qp_solve(P, q, G, h, u_lim, N, polish="exact", tol=IPM_TOL):
             pol = qp_polish_regularised(Ps, qs, Gs, hs, x, s, lam)
     if pol is not None:
         x, lam = pol
+    cs = certificate_scaled(Ps, qs, Gs, hs, x, lam)
+    if require_certificate and not cs["certified"]:
+        raise UncertifiedQP(f"QP not certified after {escalation} escalations: "
+                            + ", ".join(f"{k} {v:.2e}" for k, v in cs.items() if k != "certified"))
     z = x * sv
     lam_u = lam / rn          # multipliers of the unscaled rows
     cert = kkt_residuals(P, q, G, h, z, lam_u)
-    return QPResult(z, lam_u, it, st == 1, pol is not None, cert)
+    return QPResult(z, lam_u, it, st == 1, pol is not None, cert, cs["certified"], cs, escalation)
 
 
 # ---------------------------------------------------------------------------
@@ -1031,7 +1124,9 @@ def scp_solve(p: Problem, u_warm=None, mode="faithful", max_scp=MAX_SCP_ITER,
         if keep_history:
             hist.append(dict(u_lin=u_lin, A=A, b=b, z=res.z.copy(), obj=ev.obj,
                              maxviol=ev.max_violation, delta=delta, ipm_iters=res.iters,
-                             polished=res.polished, certificate=res.certificate))
+                             polished=res.polished, certificate=res.certificate,
+                             certified=res.certified, certificate_scaled=res.certificate_scaled,
+                             escalations=res.escalations))
         if nV == 1 and abs(delta) < DELTA_TOL and ev.max_violation > CONSTRAINT_TOL:
             conv = True
             break

@@ -87,12 +87,13 @@ _lib = None
 
 
 def load(path=None):
-    """Load the HIP library (raises OSError if it was not built)."""
+    """Load the in-tree HIP library (raises OSError if it was not built).  The product
+    path reads no environment variable: another build is loaded only by an explicit
+    ``path`` or by ``use_build`` (benchmark and tools A/B runs)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
-    # SCPQP_LIB: a diagnostic build of the same library (A/B runs of kernel variants)
-    p = path or os.environ.get("SCPQP_LIB") or LIB_PATH
+    p = path or LIB_PATH
     if not os.path.exists(p):
         raise OSError(f"scpqp: HIP library not built ({p}); run __graft_entry__.build()")
     lib = C.CDLL(p)
@@ -132,6 +133,15 @@ def load(path=None):
     if path is None:
         _lib = lib
     return lib
+
+
+def use_build(path):
+    """Tools / tests only (bench.py --lib, tools/bitwise_ab.py): make every later
+    ``load()`` of this process return another build of the same C-ABI (an A/B variant or
+    a diagnostic build), loaded before any solver is created."""
+    global _lib
+    _lib = load(os.path.abspath(path))
+    return _lib
 
 
 def check(rc, lib=None):

@@ -15,6 +15,31 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: longer CPU test")
+    lib = os.environ.get("SCPQP_TEST_LIB")
+    if lib:
+        # tests only: the suite on another build of the same C-ABI, e.g. the
+        # reduction-buffer check build (scpqp/build.py --check; checked at session end)
+        from scpqp import _lib
+        _lib.use_build(lib)
+
+
+def pytest_sessionfinish(session, exitstatus):
+    """With the reduction-check build loaded (SCPQP_TEST_LIB): every block reduction of
+    every kernel the suite ran must have used a buffer other than the previous
+    reduction's, or have had a barrier between them (scpqp_kernel.h block_reduce4)."""
+    if not os.environ.get("SCPQP_TEST_LIB"):
+        return
+    import ctypes
+    from scpqp import _lib
+    lib = _lib.load()
+    if not hasattr(lib, "scpqp_diag_reduce_check"):
+        return
+    out = (ctypes.c_ulonglong * 2)()
+    rc = lib.scpqp_diag_reduce_check(out, 0)
+    print(f"\nreduction-buffer check: rc {rc}, {out[0]} block reductions, "
+          f"{out[1]} reused the previous reduction's buffer with no barrier between them")
+    if rc != 0 or out[1] != 0 or out[0] == 0:
+        session.exitstatus = 1
 
 
 @pytest.fixture(scope="session")

@@ -182,19 +182,19 @@ def _oracle_modes_job(args):
 # Capped problems (the SCP loop ends at the reference's 20-QP cap without meeting its
 # stopping rule, SCP_controller.py:86, 191-195).  Their iterates oscillate, so rounding
 # differences that the stopping rule forgives on a converged problem are carried through
-# all 20 iterations.  Every capped problem is held, per SCP iteration it, to
-#     |u_dev(it) - u_reg(it)|   <= U_TOL                       (1e-7 rad)
-#     |u_dev(it) - u_exact(it)| <= U_TOL + |u_reg(it) - u_exact(it)|
-# where u_exact / u_reg are the restatement's two polish modes (the reference's exact KKT
-# polish and the device's regularised one, oracle/scp_reference.py).  The first line is
-# the converged-problem tolerance against the restatement of the device's own algorithm;
-# the second widens it only by the restatement's own mode-to-mode spread at that iteration
-# (the reference's answer is not pinned more tightly than that: both modes certify a KKT
-# point of the same QP).  No floor derived from the device's own results.  The final u and
-# trajectory are held the same way (U_TOL, TRAJ_TOL against the regularised mode; plus the
-# final mode spread against the exact one).  Measured (profiles/r05_capped.txt): the device
-# tracks the regularised restatement to <= 3e-9 rad at every iteration of every capped
-# problem; the mode spread reaches 2.1e-5 rad (c2 problem 323, QP 2).
+# all 20 iterations.  Every capped problem is held, at every SCP iteration it, to the
+# converged-problem tolerance against both restatement modes:
+#     |u_dev(it) - u_exact(it)| <= U_TOL   and   |u_dev(it) - u_reg(it)| <= U_TOL   (1e-7 rad)
+# where u_exact is the restatement with the reference's exact KKT polish and u_reg the one
+# with the device's regularised polish (oracle/scp_reference.py).  Every QP of both runs
+# must carry a KKT certificate (certificate_scaled; the exact mode raises UncertifiedQP
+# otherwise), so both are the QP's unique minimiser to solver accuracy.  Round
+# 5 widened the exact-mode bound by the two modes' spread; that spread (2.1e-5 rad on c2
+# problem 323) was an uncertified oracle QP (the exact polish diverged and the fallback
+# returned the IPM point, stationarity 5e-3), not reference ambiguity (verdict r05).  With
+# the safeguarded polish and the certificate check the spread is <= 3e-9 rad on a
+# 256-problem c2 sample (tools/oracle_certify_sweep.py).  The final u and trajectory are
+# held to U_TOL / TRAJ_TOL against both modes.
 
 
 def _check_capped(out, b, nV, H, r_exact, r_reg, what):
@@ -205,14 +205,16 @@ def _check_capped(out, b, nV, H, r_exact, r_reg, what):
     N = nV * H
     e_dev = e_reg = e_mode = 0.0
     for it in range(R.MAX_SCP_ITER):
+        assert r_exact.history[it]["certified"], f"{what}: exact-mode QP {it} uncertified"
+        assert r_reg.history[it]["certified"], f"{what}: regularised-mode QP {it} uncertified"
         zd = tr[it]["z"][:N]
         ed = float(np.max(np.abs(zd - r_exact.history[it]["z"][:N])))
         er = float(np.max(np.abs(zd - r_reg.history[it]["z"][:N])))
         em = float(np.max(np.abs(r_reg.history[it]["z"][:N] - r_exact.history[it]["z"][:N])))
         assert er <= SP.U_TOL, \
             f"{what}: iteration {it} |u - u_reg| {er:.2e} rad"
-        assert ed <= SP.U_TOL + em, \
-            f"{what}: iteration {it} |u - u_exact| {ed:.2e} rad, restatement mode spread {em:.2e}"
+        assert ed <= SP.U_TOL, \
+            f"{what}: iteration {it} |u - u_exact| {ed:.2e} rad (restatement mode spread {em:.2e})"
         e_dev, e_reg, e_mode = max(e_dev, ed), max(e_reg, er), max(e_mode, em)
     ub, tb = (t.cpu().numpy() for t in unpack_problem(out, b, nV, H))
     e_u = float(np.max(np.abs(ub - r_exact.u)))
@@ -224,13 +226,14 @@ def _check_capped(out, b, nV, H, r_exact, r_reg, what):
     print(f"{what}: per-iteration |u - u_exact| {e_dev:.2e} |u - u_reg| {e_reg:.2e} rad; final "
           f"|u - u_reg| {r_u:.2e} rad |traj - traj_reg| {r_t:.2e} m; mode spread {e_mode:.2e} rad")
     assert r_u <= SP.U_TOL and r_t <= SP.TRAJ_TOL, what
-    assert e_u <= SP.U_TOL + m_u and e_t <= SP.TRAJ_TOL + m_t, what
+    assert e_u <= SP.U_TOL and e_t <= SP.TRAJ_TOL, (what, e_u, e_t, m_u, m_t)
     return e_dev, e_mode
 
 
 def test_capped_problems_within_stated_tolerance(gpu):
     """Every capped problem of the c2 batch (B = 1024) and of the first 32 problems of the
-    c3 stream, per SCP iteration against both restatement modes (contract above).
+    c3 stream, per SCP iteration against both certified restatement modes at 1e-7 rad
+    (contract above).
     Problems 14 and 18 of the c3 stream, whose two restatement modes agree to 2e-10 m over
     all 20 iterations, are held to the converged-problem tolerances (1e-7 rad)."""
     worst = {}

@@ -1,5 +1,5 @@
 """Bitwise A/B of two builds of the library on one configuration: solve the same batch
-with each (one process per library, SCPQP_LIB) and compare every output array exactly.
+with each (one process per library, _lib.use_build) and compare every output array exactly.
 
     python tools/bitwise_ab.py <config c2|c4|c5|c3> <lib_a.so> <lib_b.so> [batch]
 """
@@ -17,9 +17,11 @@ CFG = {"c2": (4, 20, 1024, None), "c4": (4, 20, 8192, None), "c3": (8, 30, 4096,
        "c5": (4, 30, 3072, (10, 20, 30))}
 
 
-def run_one(cfg, out_path, batch):
+def run_one(cfg, out_path, batch, lib):
     import torch
     import Scenarios
+    from scpqp import _lib
+    _lib.use_build(lib)
     from scpqp import shard
     from scpqp.solver import ScpQpSolver
     nv, hp, B, mixed = CFG[cfg]
@@ -40,7 +42,7 @@ def run_one(cfg, out_path, batch):
 
 def main():
     if sys.argv[1] == "--one":
-        run_one(sys.argv[2], sys.argv[3], int(sys.argv[4]) if len(sys.argv) > 4 else 0)
+        run_one(sys.argv[2], sys.argv[3], int(sys.argv[4]), sys.argv[5])
         return
     cfg, la, lb = sys.argv[1:4]
     batch = sys.argv[4] if len(sys.argv) > 4 else "0"
@@ -48,8 +50,8 @@ def main():
     for lib in (la, lb):
         fd, path = tempfile.mkstemp(suffix=".npz")
         os.close(fd)
-        env = dict(os.environ, SCPQP_LIB=os.path.abspath(lib))
-        subprocess.run([sys.executable, __file__, "--one", cfg, path, batch], env=env, check=True)
+        subprocess.run([sys.executable, __file__, "--one", cfg, path, batch, os.path.abspath(lib)],
+                       check=True)
         res.append(dict(np.load(path)))
         os.unlink(path)
     same = True

@@ -56,7 +56,7 @@ for st in "$@"; do
                 for ent in ${libs//,/ }; do
                     lib=${ent##*@}; envs=""; [ "$ent" != "$lib" ] && envs=${ent%%@*}
                     [ "${lib:0:1}" = / ] || lib=$PWD/$lib
-                    run ab 300 env $envs SCPQP_LIB=$lib python bench.py --no-cpu --config $c --steps $n --warmup 1
+                    run ab 300 env $envs python bench.py --lib $lib --no-cpu --config $c --steps $n --warmup 1
                     grep '^{' $OUT/ab.log | line "$c $ent" | tee -a $OUT/ab.txt
                 done
             done

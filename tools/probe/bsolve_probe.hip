@@ -2,8 +2,7 @@
 // with inverted 4 x 4 / 8 x 8 diagonal blocks (BSolver), n compile-time as in the c2
 // kernel (81) and c5's Hp 30 (121).  One workgroup alone, 1 and 2 per CU.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/probe/bsolve_probe.hip -o tools/probe/bsolve_probe
-#define SCPQP_DIAG_NO_HOST
-#include "../../senquential-convex-programming-for-trajectory-planning_amd/csrc/scpqp.hip"
+#include "../../senquential-convex-programming-for-trajectory-planning_amd/csrc/scpqp_kernel.h"
 
 #include <vector>
 

@@ -2,8 +2,7 @@
 // csrc/scpqp.hip, host side left out): cycles per factorisation of an SPD
 // matrix of order n in the packed LDS layout, alone and 3 workgroups per CU.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/probe/chol_probe.hip -o tools/probe/chol_probe
-#define SCPQP_DIAG_NO_HOST
-#include "../../senquential-convex-programming-for-trajectory-planning_amd/csrc/scpqp.hip"
+#include "../../senquential-convex-programming-for-trajectory-planning_amd/csrc/scpqp_kernel.h"
 #include <vector>
 
 namespace {
