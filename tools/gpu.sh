@@ -3,6 +3,9 @@
 #   gpurun --timeout 1500 -- bash tools/gpu.sh <tag> <step> [<step> ...]
 # Steps (each argument one step; values after ':' separated by ','):
 #   tests[:k-expr]        GPU test suite (one pytest process), optionally -k filtered
+#   checktests[:k-expr]   the GPU suite on the reduction-check build (SCPQP_TEST_LIB, build.py --check)
+#   reducecheck:<lib>     reduction-buffer counters of a check build over the configs (records a FAIL
+#                         without stopping the chain; a crash still stops it)
 #   smoke                 __graft_entry__.smoke()
 #   bench:<cfg>[,steps]   bench.py line of one BASELINE configuration (c2 with the CPU leg)
 #   ab:<cfgs>:<libs>[:reps]  A/B of library builds, e.g. ab:c2/10,c4/3:scpqp/libscpqp.so,/tmp/x.so:2
@@ -39,12 +42,24 @@ for st in "$@"; do
         [ -n "$rest" ] && ARGS+=(-k "$rest")
         run pytest 1100 python -u -m pytest "${ARGS[@]}"
         grep -E "passed|failed" $OUT/pytest.log | tail -2 ;;
+    checktests)
+        ARGS=(tests -m gpu -v -x -s -p no:cacheprovider --timeout 300 --timeout-method thread)
+        [ -n "$rest" ] && ARGS+=(-k "$rest")
+        run checktests 1100 env SCPQP_TEST_LIB=$PWD/$PKG/scpqp/libscpqp_check.so python -u -m pytest "${ARGS[@]}"
+        grep -E "passed|failed|reduction-buffer" $OUT/checktests.log | tail -3 ;;
+    reducecheck)
+        lib=$rest; [ "${lib:0:1}" = / ] || lib=$PWD/$lib
+        name=reducecheck_$(basename $lib .so)
+        echo "== $name ($(date +%T))"
+        timeout -k 10 300 python tools/reduce_check.py $lib > $OUT/$name.log 2>&1; rc=$?
+        tail -7 $OUT/$name.log
+        if [ $rc -gt 1 ]; then echo "!! $name rc=$rc"; exit $rc; fi ;;
     smoke)
         run smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
         tail -1 $OUT/smoke.log ;;
     bench)
         cfg=${rest%%,*}; steps=""; [ "$cfg" != "$rest" ] && steps="--steps ${rest#*,} --warmup 1"
-        extra="--no-cpu"; [ "$cfg" = c2 ] && extra=""
+        extra=""   # every config with its CPU leg and parity sample (verdict r05 item 6)
         run bench_$cfg 600 python bench.py --config $cfg $steps $extra
         grep '^{' $OUT/bench_$cfg.log > $OUT/bench_$cfg.json
         line $cfg < $OUT/bench_$cfg.json ;;
