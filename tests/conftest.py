@@ -15,12 +15,6 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
     config.addinivalue_line("markers", "slow: longer CPU test")
-    lib = os.environ.get("SCPQP_TEST_LIB")
-    if lib:
-        # tests only: the suite on another build of the same C-ABI, e.g. the
-        # reduction-buffer check build (scpqp/build.py --check; checked at session end)
-        from scpqp import _lib
-        _lib.use_build(lib)
 
 
 def pytest_sessionfinish(session, exitstatus):
@@ -31,6 +25,8 @@ def pytest_sessionfinish(session, exitstatus):
         return
     import ctypes
     from scpqp import _lib
+    if _lib._lib is None:
+        return
     lib = _lib.load()
     if not hasattr(lib, "scpqp_diag_reduce_check"):
         return
@@ -54,5 +50,10 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.fail("gpu test selected but torch.cuda.is_available() is False")
     from scpqp import _lib
+    if os.environ.get("SCPQP_TEST_LIB"):
+        # tests only: the suite on another build of the same C-ABI, e.g. the
+        # reduction-buffer check build (scpqp/build.py --check; checked at session end),
+        # loaded once the GPU runtime is up
+        _lib.use_build(os.environ["SCPQP_TEST_LIB"])
     _lib.load()          # raises if libscpqp.so is missing: no fallback path exists
     return torch.device("cuda", 0)
