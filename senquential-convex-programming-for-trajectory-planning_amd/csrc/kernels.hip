@@ -19,6 +19,9 @@ template int scpqp_kern::diag_read<SCPQP_KGROUP>(int, unsigned long long*, int, 
 
 #if SCPQP_KGROUP == 1   // c2 / c4: 4 vehicles, Hp 20, plan 1 at three workgroups per CU
 SCPQP_INST(false, true, 2, 3, 1)
+#ifdef SCPQP_DIAG   // diagnostic builds: the lean plan at four per CU (scpqp.hip plan)
+SCPQP_INST(false, true, 2, 4, 1)
+#endif
 #elif SCPQP_KGROUP == 2   // c3: 8 vehicles, Hp 30, factor in the workspace
 SCPQP_INST(true, true, 4, 2, 3)
 #elif SCPQP_KGROUP == 3   // c5: mixed horizons up to 30, lean plan 1 at two per CU

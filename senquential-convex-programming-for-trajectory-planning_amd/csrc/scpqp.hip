@@ -19,6 +19,9 @@
 #define SCPQP_EXTERN_LAUNCH(HG, VG, RM, OCC, SH) \
     extern template int scpqp_kern::launch<HG, VG, RM, OCC, SH>(const void*, size_t, hipStream_t, int);
 SCPQP_KERNEL_LIST(SCPQP_EXTERN_LAUNCH)
+#ifdef SCPQP_DIAG
+SCPQP_EXTERN_LAUNCH(false, true, 2, 4, 1)   // the OCC = 4 residency experiment (plan)
+#endif
 #undef SCPQP_EXTERN_LAUNCH
 // kernels.hip's groups, each with its own diagnostic counters (diag_read<group>)
 constexpr int kKernelGroups = 10;
@@ -142,6 +145,22 @@ int plan(scpqp_handle* h) {
             }
         }
     }
+#ifdef SCPQP_DIAG
+    // diagnostic build: SCPQP_OCC4=1 runs the lean plan 1 at four workgroups per CU (the
+    // 128-VGPR budget of OCC = 4) when it fits (the round-6 c2 residency experiment)
+    if (const char* o4 = getenv("SCPQP_OCC4")) {
+        const Off f = plan_offsets(V, O, Hm, false, true, true);
+        if (atoi(o4) == 1 && (size_t)(f.persist + f.uni) * sizeof(double) * 4 <= kLdsLimit) {
+            h->hG = 0;
+            h->vG = 1;
+            h->ldsBytes = (size_t)(f.persist + f.uni) * sizeof(double);
+            h->wsStride = f.ws;
+            h->grid = h->cus * 4;
+            h->occ = 4;
+            return 0;
+        }
+    }
+#endif
     if (best < 0) return fail(SCPQP_E_SIZE, "problem too large for the LDS plan%s");
     const Off f = plan_offsets(V, O, Hm, best >= 2, best >= 1, bestLean);
     h->hG = best >= 2;
@@ -229,6 +248,9 @@ int launch(scpqp_handle* h, KArgs& a, hipStream_t st) {
         if (atoi(e) == 0) sh = 0;
 #endif
     if (sh == 1 && !h->hG && h->vG && R == 2 && occ == 3) return SCPQP_RUN(false, true, 2, 3, 1);
+#ifdef SCPQP_DIAG
+    if (sh == 1 && !h->hG && h->vG && R == 2 && occ == 4) return SCPQP_RUN(false, true, 2, 4, 1);
+#endif
     if (sh == 2 && h->vG && R == 2 && occ == 3) {
         if (h->hG) return SCPQP_RUN(true, true, 2, 3, 2);
         return SCPQP_RUN(false, true, 2, 3, 2);

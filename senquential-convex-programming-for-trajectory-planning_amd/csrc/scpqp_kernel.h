@@ -169,6 +169,21 @@ __host__ __device__ inline int trace_stride(int V, int O, int Hm) {
 // padded to an even length so every row starts 16-byte aligned.
 __host__ __device__ __forceinline__ int roff(int i) { return i * (i + 1) / 2 + ((i + 1) >> 1); }
 
+// The reduction / slot area `red` of a plan (doubles): [0, 48) the three partial-sum
+// buffers of block_reduce4, [0, 64) also the factorisation's look-ahead rows (ldbuf; no
+// reduction runs inside the factorisation), then single slots, then the pivots.
+constexpr int kRedFlag = 64;    // factorisation failure flag, 2 ints [step parity]
+constexpr int kIdlSlot = 65;    // 1 / polish delta of the current polish round
+constexpr int kWorkSlot = 66;   // the problem index taken from the work queue (int)
+constexpr int kLeadSlot = 67;   // lead election (2 ints)
+constexpr int kOrSlot = 68;     // workgroup OR of the sampler's quirk flags (int)
+constexpr int kPivSlot = 72;    // pivots [step mod 2G][CB] (G = 4 panels per group on
+                                // workspace factors, else 1; CB = 8)
+__host__ __device__ constexpr int red_size(bool hG) { return kPivSlot + 2 * (hG ? 4 : 1) * 8; }
+// the lean plan 1 (W~ blocks and constraint rows in the workspace beside the vectors) at
+// two workgroups per CU (c5, Hp 30), or four (the round-6 c2 residency experiment)
+__host__ __device__ constexpr bool lean_plan(bool hG, bool vG, int occ) { return !hG && vG && (occ == 2 || occ == 4); }
+
 struct Off {
     int x0, u0, ec, g, p0, ref, ob, ub, pb, ya, yb, qs, rowE, rowW, rowH, rinfo;
     int z, dz, rhs, rd, dinv, red, scr;
@@ -184,7 +199,11 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     const int N = V * Hm, n = N + 1, m = V * (V - 1) / 2 * Hm + V * O * Hm;
     const int mc = m + 2 * N + 1, ld = n + ((6 - n % 4) % 4), nb = V * (V + 1) / 2;
     Off f;
+#ifdef SCPQP_DIAG_REDUCE_CHECK
+    int p = 2;   // smem_[0]: the reduction-buffer check's slot (bar)
+#else
     int p = 0;
+#endif
     f.x0 = p; p += pad2(6 * V);
     f.u0 = p; p += pad2(V);
     f.ec = p; p += pad2(2 * V);
@@ -208,7 +227,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.rhs = p; p += pad2(n);
     f.rd = p; p += pad2(n);
     f.dinv = p; p += pad2(n);
-    f.red = p; p += 192;   // [0,64) reductions, 120 flag, 124 work slot, 126 lead, [128,192) pivots
+    f.red = p; p += red_size(hG);   // kRedFlag ... kPivSlot
     f.persist = p;
     f.scr = p;
     int u = 0;
@@ -246,7 +265,7 @@ struct Lay {
     ldouble *x0, *u0, *ec, *g, *p0, *ref, *ob, *ub, *pb, *ya, *yb, *qs;
     ldouble *z, *dz, *rhs, *rd, *dinv, *red, *scr;
     // lean plan 1 (two workgroups per CU): W~ and the constraint rows in the workspace
-    static constexpr bool LEAN = !HG && VG && OCC == 2;
+    static constexpr bool LEAN = lean_plan(HG, VG, OCC);
     // W~ blocks: in the workspace on plan 2 for factors of 4 row slots (plan_offsets)
     static constexpr bool WGLOBAL = (HG && VG && RM == 4) || LEAN;
     using WT = typename std::conditional<WGLOBAL, gdouble, ldouble>::type;
@@ -371,18 +390,21 @@ __device__ __forceinline__ double wave_sum(double v) { return wave_reduce<false>
 __device__ __forceinline__ double wave_max(double v) { return wave_reduce<true>(v); }
 
 // Workgroup barrier.  Diagnostic build -DSCPQP_DIAG_REDUCE_CHECK: thread 0 also records
-// that a barrier ran since the last block reduction (block_reduce4's buffer check).
+// that a barrier ran since the last block reduction (block_reduce4's buffer check), in the
+// first slot of the dynamic LDS, which that build's plans reserve (plan_offsets).  (A
+// static __shared__ variable beside the dynamic LDS, the first form of this check, faulted
+// on the device: the plans assume the dynamic LDS starts at offset 0.)
 #ifdef SCPQP_DIAG_REDUCE_CHECK
 // [reductions checked, reductions whose buffer equals the previous reduction's with no
 // barrier between them] (read by scpqp_diag_reduce_check)
 __device__ unsigned g_redchk[2];
-__shared__ int s_redchk_last;   // buffer of the last reduction, -1 after a barrier (thread 0)
+__device__ __forceinline__ lint& redchk_last() { return ((lint*)smem_)[0]; }
 __device__ __forceinline__ void bar() {
-    bar();
-    if (threadIdx.x == 0) s_redchk_last = -1;
+    __syncthreads();
+    if (threadIdx.x == 0) redchk_last() = -1;
 }
 #else
-__device__ __forceinline__ void bar() { bar(); }
+__device__ __forceinline__ void bar() { __syncthreads(); }
 #endif
 
 // Reduce four values across the workgroup; bit q of maxmask: max, else sum.
@@ -407,7 +429,7 @@ __device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldoub
 #ifdef SCPQP_DIAG_REDUCE_CHECK
     if (threadIdx.x == 0) {
         atomicAdd(&g_redchk[0], 1u);
-        if (s_redchk_last == BUF) atomicAdd(&g_redchk[1], 1u);
+        if (redchk_last() == BUF) atomicAdd(&g_redchk[1], 1u);
     }
 #endif
     if (l == 0) {
@@ -416,7 +438,7 @@ __device__ __forceinline__ void block_reduce4(double (&v)[4], int maxmask, ldoub
     }
     __syncthreads();
 #ifdef SCPQP_DIAG_REDUCE_CHECK
-    if (threadIdx.x == 0) s_redchk_last = BUF;
+    if (threadIdx.x == 0) redchk_last() = BUF;
 #endif
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -852,7 +874,7 @@ __device__ __noinline__ int setup_problem_ni(const cKArgs* ap, gdouble* ws, int 
     Hb = __builtin_amdgcn_readfirstlane(Hb);
     const cKArgs& a = *ap;
     const cParams& P = *(const cParams*)a.P;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, lean_plan(HG, VG, OCC));
     const Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, ws, f, P.nV, P.nO, Hb);
     return setup_problem(a, P, L, b);
 }
@@ -1561,16 +1583,17 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
 // panels per grouped trailing update: 4 since round 5 (c3 +1-2 % against 2 in one session,
 // HBM traffic 2.93 -> 2.35 TB per launch; unsplit in round 2 it measured slower)
 constexpr int kGroup = 4;
-static_assert(2 * kGroup * CB <= 64, "the pivot buffer holds 64 entries");
+static_assert(kPivSlot + 2 * kGroup * CB == red_size(true) && kPivSlot + 2 * CB == red_size(false),
+              "the pivot buffer of red_size");
 
 template <class LT>
 __device__ bool cholesky(const LT& L) {
     const int n = __builtin_amdgcn_readfirstlane(L.n);
     constexpr int RS = LT::RMAX;   // row slots per lane in the panel
     constexpr int G = LT::HGLOBAL ? kGroup : 1;
-    lint* flag = (lint*)(L.red + 120);   // [step parity]
+    lint* flag = (lint*)(L.red + kRedFlag);   // [step parity]
     ldouble* ldbuf = L.red;              // [CB][CB] look-ahead rows (panel_factor; red is idle here)
-    ldouble* dbuf = L.red + 128;         // pivots [step mod 2G][CB]; a group's slots are adjacent
+    ldouble* dbuf = L.red + kPivSlot;    // pivots [step mod 2G][CB]; a group's slots are adjacent
     PROF_T0();
     for (int r0 = 0, s = 0; r0 < n; r0 += CB, ++s) {
         const int par = s & 1;
@@ -2033,7 +2056,6 @@ constexpr double kPolishTol = 1e-9;
 // The polish penalty (warm and cold rounds alike) is polish_delta; 1/delta of the
 // current round lives in red[kIdlSlot] (set by the prep phases).  A separate warm
 // penalty was measured and not kept.
-constexpr int kIdlSlot = 122;
 __device__ __forceinline__ int polish_stop(const D4& d, int ref, double early) {
     if (ref < 1) return 0;
     if (d.a <= kPolishTol * fmax(1.0, d.b)) return 1;
@@ -2056,7 +2078,7 @@ __device__ __forceinline__ Ctx uniform_ctx(const Ctx& c) {
 
 template <bool HG, bool VG, int RM, int OCC, int SH>
 __device__ __forceinline__ Lay<HG, VG, RM, OCC> lay_of(const Ctx& c) {
-    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeHM<SH>(c.P->hpMax), HG, VG, !HG && VG && OCC == 2);
+    const Off f = plan_offsets(shapeV<SH>(c.P->nV), shapeO<SH>(c.P->nO), shapeHM<SH>(c.P->hpMax), HG, VG, lean_plan(HG, VG, OCC));
     Lay<HG, VG, RM, OCC> L = make_lay<HG, VG, RM, OCC, SH>((ldouble*)smem_, c.ws, f, c.P->nV, c.P->nO, c.Hb);
     L.lead = c.lead;
     return L;
@@ -2688,15 +2710,16 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
     const cParams& P = *(const cParams*)a.P;
     const int tid = threadIdx.x;
     gdouble* ws = a.ws ? (gdouble*)a.ws + (size_t)blockIdx.x * a.wsStride : nullptr;
-    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, !HG && VG && OCC == 2);
-    lint* slot = (lint*)(smem + f.red + 124);
+    const Off f = plan_offsets(shapeV<SH>(P.nV), shapeO<SH>(P.nO), shapeHM<SH>(P.hpMax), HG, VG, lean_plan(HG, VG, OCC));
+    lint* slot = (lint*)(smem + f.red + kWorkSlot);
+    lint* orslot = (lint*)(smem + f.red + kOrSlot);
     ldouble* lub = smem + f.ub;   // u-bar
     ldouble* lpb = smem + f.pb;   // positions of the last evaluated u
     ldouble* lref = smem + f.ref;
     ldouble* lg = smem + f.g;
     ldouble* lp0 = smem + f.p0;
     ldouble* lqs = smem + f.qs;
-    const int lead = lead_wave_elect((lint*)(smem + f.red + 126));
+    const int lead = lead_wave_elect((lint*)(smem + f.red + kLeadSlot));
     for (;;) {
         if (tid == 0) {
             const int w = atomicAdd(a.counter, 1);
@@ -2727,9 +2750,14 @@ __global__ __launch_bounds__(NT, OCC) void scp_kernel(KArgs a) {
         if (tid == 0 && b < 8192) g_ptime[2 * b] = __builtin_amdgcn_s_memrealtime();
 #endif
         PROF_T0();
+        // the sampler's flags, ORed over the workgroup in an LDS slot (__syncthreads_or
+        // would add 256 B of static LDS to every plan)
+        if (tid == 0) *orslot = 0;
         const int sflag = setup_problem_ni<HG, VG, RM, OCC, SH>((const cKArgs*)__builtin_amdgcn_kernarg_segment_ptr(), ws, b, Hb);
         PROF_ACC(10);
-        const int sflag_any = __syncthreads_or(sflag);
+        if (sflag) *orslot = 1;
+        bar();
+        const int sflag_any = *orslot;
         const size_t slotU = (size_t)b * V * P.hpMax;   // [B][V*Hmax] slots
         if (a.mode == MODE_SAMPLE) {
             for (int i = tid; i < Hb * 2 * V; i += NT) {
