@@ -91,7 +91,18 @@ def oracle_job(args):
         if p not in sys.path:
             sys.path.insert(0, p)
     from oracle import scp_reference as R_
+    single_thread_blas()
     n_veh, hp, x0, u0, ec = args[:5]
     sc = R_.circle_scenario(n_veh, Hp=args[5] if len(args) > 5 else hp)
     p = R_.make_problem(sc, x0, u0, ec, Hp=hp)
     return R_.scp_solve(p, mode="structured", keep_history=True)
+
+
+def single_thread_blas():
+    """One BLAS thread in a pool worker (the pools run one worker per core of the box's
+    CPU share; a multithreaded BLAS per worker on small matrices oversubscribes it)."""
+    try:
+        import threadpoolctl
+        threadpoolctl.threadpool_limits(1)
+    except ImportError:
+        pass

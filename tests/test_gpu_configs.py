@@ -172,6 +172,7 @@ def _oracle_modes_job(args):
         if p not in sys.path:
             sys.path.insert(0, p)
     from oracle import scp_reference as R_
+    SP.single_thread_blas()
     n_veh, hp, x0, u0, ec = args[:5]
     sc = R_.circle_scenario(n_veh, Hp=hp)
     p = R_.make_problem(sc, x0, u0, ec, Hp=hp)

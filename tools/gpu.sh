@@ -38,12 +38,12 @@ for st in "$@"; do
     kind=${st%%:*}; rest=""; [ "$kind" != "$st" ] && rest=${st#*:}
     case $kind in
     tests)
-        ARGS=(tests -m gpu -v -x -p no:cacheprovider --timeout 300 --timeout-method thread)
+        ARGS=(tests -m gpu -v -x -p no:cacheprovider --timeout 170 --timeout-method thread)
         [ -n "$rest" ] && ARGS+=(-k "$rest")
         run pytest 1100 python -u -m pytest "${ARGS[@]}"
         grep -E "passed|failed" $OUT/pytest.log | tail -2 ;;
     checktests)
-        ARGS=(tests -m gpu -v -x -s -p no:cacheprovider --timeout 300 --timeout-method thread)
+        ARGS=(tests -m gpu -v -x -s -p no:cacheprovider --timeout 170 --timeout-method thread)
         [ -n "$rest" ] && ARGS+=(-k "$rest")
         run checktests 1100 env SCPQP_TEST_LIB=$PWD/$PKG/scpqp/libscpqp_check.so python -u -m pytest "${ARGS[@]}"
         grep -E "passed|failed|reduction-buffer" $OUT/checktests.log | tail -3 ;;
