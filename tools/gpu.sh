@@ -10,8 +10,8 @@
 #   bench:<cfg>[,steps]   bench.py line of one BASELINE configuration (c2 with the CPU leg)
 #   ab:<cfgs>:<libs>[:reps]  A/B of library builds, e.g. ab:c2/10,c4/3:scpqp/libscpqp.so,/tmp/x.so:2
 #                         (bench.py --no-cpu, alternating; VAR=value@lib.so sets an env var)
-#   phases:<lib>[:cfgs]   phase stamps of a -DSCPQP_PROF build (tools/gpu_prof.py), cfgs as 4/20/1
-#   timeline:<lib>        per-problem start/end of a -DSCPQP_PROF build (c2, B = 1024)
+#   phases:[VAR=v@]<lib>[:cfgs]  phase stamps of a -DSCPQP_PROF build (tools/gpu_prof.py), cfgs as 4/20/1
+#   timeline:[VAR=v@]<lib>       per-problem start/end of a -DSCPQP_PROF build (c2, B = 1024)
 #   stats:<cfg>           rocprofv3 --kernel-trace --stats of the bench
 #   pmc:<cfg>             SQ, MFMA, FETCH_SIZE and WRITE_SIZE passes, each its own rocprofv3 run
 #   rollout               closed-loop rollout throughput (tools/bench_rollout.py)
@@ -77,15 +77,18 @@ for st in "$@"; do
             done
         done ;;
     phases)
-        lib=${rest%%:*}; cfgs="4:20:1"; [ "$lib" != "$rest" ] && cfgs=$(echo ${rest#*:} | tr ',/' ' :')
+        ent=${rest%%:*}; cfgs="4:20:1"; [ "$ent" != "$rest" ] && cfgs=$(echo ${rest#*:} | tr ',/' ' :')
+        lib=${ent##*@}; envs=""; [ "$ent" != "$lib" ] && envs=${ent%%@*}
         [ "${lib:0:1}" = / ] || lib=$PWD/$lib
-        name=phases_$(basename $lib .so)
-        run $name 300 env SCPQP_PROF_LIB=$lib python tools/gpu_prof.py $cfgs
+        name=phases_$(basename $lib .so)${envs:+_${envs%%=*}}
+        run $name 300 env $envs SCPQP_PROF_LIB=$lib python tools/gpu_prof.py $cfgs
         grep -v amdgpu.ids $OUT/$name.log ;;
     timeline)
-        lib=$rest; [ "${lib:0:1}" = / ] || lib=$PWD/$lib
-        run timeline 300 env SCPQP_PROF_LIB=$lib python tools/gpu_timeline.py 1024
-        head -20 $OUT/timeline.log ;;
+        ent=$rest; lib=${ent##*@}; envs=""; [ "$ent" != "$lib" ] && envs=${ent%%@*}
+        [ "${lib:0:1}" = / ] || lib=$PWD/$lib
+        name=timeline${envs:+_${envs%%=*}}
+        run $name 300 env $envs SCPQP_PROF_LIB=$lib python tools/gpu_timeline.py 1024
+        head -20 $OUT/$name.log ;;
     stats)
         c=$rest; steps=5; [ $c = c3 ] && steps=2; [ $c = c2 ] && steps=10
         run stats_$c 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/stats_$c -o run -- python3 bench.py --config $c --steps $steps --warmup 2 --no-cpu
