@@ -44,9 +44,18 @@ import numpy as np  # noqa: E402
 FP64_PEAK_TFLOPS = 78.6   # MI355X dense FP64 (vector == MFMA on gfx950), AMD datasheet
 HBM_PEAK_GBS = 8000.0
 METRIC = "SCP-QP solves/sec/GPU (4 veh, Hp=20); traj ℓ∞ err vs CVXOPT"
-# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu.sh pmc + pmc_summary.py)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05_pmc_traffic_{}.json")
-PMC_SQ = os.path.join(ROOT, "profiles", "r05_pmc_sq_{}.json")
+# committed rocprofv3 PMC summaries of the shipped kernel (tools/gpu.sh pmc + pmc_summary.py):
+# the newest round's record of each configuration
+PMC_ROUNDS = ("r06", "r05")
+
+
+def pmc_record(kind, config):
+    """profiles/<round>_pmc_<kind>_<config>.json of the newest round that has one."""
+    for rnd in PMC_ROUNDS:
+        p = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{kind}_{config}.json")
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", f"{PMC_ROUNDS[0]}_pmc_{kind}_{config}.json")
 
 
 # ----------------------------------------------------------------------------- CPU baseline
@@ -394,8 +403,8 @@ def main():
     # workload at its default batch (tools/gpu.sh pmc + tools/pmc_summary.py)
     traffic, traffic_raw, sq = None, None, None
     default_b = {"c2": 1024, "c3": 4096, "c4": 8192, "c5": 3072}[args.config]
-    tpath = PMC_TRAFFIC.format(args.config)
-    spath = PMC_SQ.format(args.config)
+    tpath = pmc_record("traffic", args.config)
+    spath = pmc_record("sq", args.config)
     if B == default_b and os.path.exists(tpath):
         try:
             with open(tpath) as fh:

@@ -320,3 +320,34 @@ def test_iteration_log_keys_and_formulas():
             assert np.allclose(log["U"][it][:, 0, v], u[v * Hp:(v + 1) * Hp])
         pu = log["prev_u"][it].reshape(-1)
         assert np.allclose(log["prevU"][it][:, 0, 0], pu[:Hp])
+
+
+@pytest.mark.parametrize("config", ["c2", "c3", "c4", "c5"])
+def test_round6_bench_records_carry_cpu_baseline_and_parity(config):
+    """Verdict r05 item 6: every configuration's committed bench line carries the CPU
+    baseline, the trajectory parity sample, the median step time beside the mean
+     and the iteration maxima."""
+    import json
+    with open(os.path.join(ROOT, "profiles", f"r06_bench_{config}.json")) as fh:
+        d = json.load(fh)
+    blk = d["cpu_baseline"]
+    assert blk["value"] > 0 and blk["cores"] >= 1 and blk["kind"] == "port" and blk["sample"]
+    assert d["traj_linf_err"] is not None and d["traj_linf_err"] <= 1e-6
+    assert d["ms_per_step_median"] > 0 and d["ms_per_step"] > 0
+    assert 1 <= d["max_scp_iters"] <= 20 and d["max_ipm_iters_per_problem"] >= 1
+    assert d["roofline"]["frac"] > 0 and d["value"] > 0
+
+
+def test_traffic_record_registers_from_the_code_object():
+    """Verdict r05 item 3: the c2 traffic record carries the descriptor's VGPR count and
+    stack size (tools/kernel_resources.py), and the stack is back at <= 260 B per lane."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    path = bench.pmc_record("traffic", "c2")
+    assert os.path.basename(path).startswith("r06_")
+    with open(path) as fh:
+        tj = json.load(fh)
+    co = tj["code_object"]
+    assert co["vgpr_count"] > 128 and co["private_segment_fixed_size"] <= 260
+    assert tj["hbm_bytes_per_launch"] <= 4.3e9

@@ -5,12 +5,21 @@ FETCH_SIZE / WRITE_SIZE are in KiB (counter_defs.yaml).  Per MI355X_MICROARCH.md
 gfx950, so it is doubled; WRITE_SIZE is taken as is.  Output: per-launch HBM
 bytes of the kernel, written as JSON (bench.py reads ``hbm_bytes_per_launch``).
 
-    python tools/pmc_summary.py gpurun_out/rXX/pmc_fetch.csv gpurun_out/rXX/pmc_write.csv out.json
+    python tools/pmc_summary.py gpurun_out/rXX/pmc_fetch.csv gpurun_out/rXX/pmc_write.csv out.json [lib.so]
+
+The register and stack fields come from the kernel's code object (tools/kernel_resources.py:
+the descriptor's .vgpr_count, .agpr_count, .vgpr_spill_count, .private_segment_fixed_size), not
+from the rocprofv3 CSV, whose VGPR_Count column is in allocation granules (round 5 recorded
+"vgpr": 84 for a 166-VGPR kernel, verdict r05).
 """
 import csv
 import json
+import os
 import statistics
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import kernel_resources as KR  # noqa: E402
 
 
 def per_dispatch(path, counter, kernel="scp_kernel"):
@@ -28,7 +37,24 @@ def per_dispatch(path, counter, kernel="scp_kernel"):
     return vals, meta
 
 
+def code_object(lib, rocprof_name):
+    """The kernel's descriptor fields from the library's code objects (None if absent)."""
+    tmpl = rocprof_name.split("scp_kernel<", 1)[-1].split(">", 1)[0].replace(" ", "")
+    try:
+        ks = KR.kernels(lib)
+    except (OSError, ValueError):
+        return None
+    names = KR.demangle([k["name"] for k in ks])
+    for k, d in zip(ks, names):
+        if "scp_kernel<" in d and d.split("scp_kernel<", 1)[1].split(">", 1)[0].replace(" ", "") == tmpl:
+            return {f: k.get(f) for f in ("vgpr_count", "agpr_count", "sgpr_count", "vgpr_spill_count",
+                                          "sgpr_spill_count", "private_segment_fixed_size",
+                                          "group_segment_fixed_size")}
+    return None
+
+
 def main():
+    lib = sys.argv[4] if len(sys.argv) > 4 else KR.LIB
     fetch, meta = per_dispatch(sys.argv[1], "FETCH_SIZE")
     write, _ = per_dispatch(sys.argv[2], "WRITE_SIZE")
     f_kib = statistics.median(fetch.values())
@@ -43,7 +69,8 @@ def main():
         "correction": "FETCH_SIZE x2 (gfx950 half-count of wide reads, MI355X_MICROARCH.md HBM); "
                       "WRITE_SIZE as is; KiB -> bytes x1024",
         "grid_threads": m["grid"], "workgroup": m["wg"], "lds_bytes": m["lds"],
-        "vgpr": m["vgpr"], "agpr": m["agpr"], "sgpr": m["sgpr"], "scratch": m["scratch"],
+        "rocprof_vgpr_granule_field": m["vgpr"], "scratch": m["scratch"],
+        "code_object": code_object(lib, m["name"]),
     }
     with open(sys.argv[3], "w") as fh:
         json.dump(out, fh, indent=1)
