@@ -169,31 +169,6 @@ __host__ __device__ inline int trace_stride(int V, int O, int Hm) {
 // padded to an even length so every row starts 16-byte aligned.
 __host__ __device__ __forceinline__ int roff(int i) { return i * (i + 1) / 2 + ((i + 1) >> 1); }
 
-// Factors in the global workspace (plan 2) are stored tile-major (round 6): the lower
-// triangle of 16 x 16 tiles, tile (I, J <= I) at I (I + 1) / 2 + J, 256 contiguous doubles
-// each (row-major), so that a 16 x 16 MFMA tile of the trailing update is 16 aligned
-// 128-byte lines (a packed row starts at any 16-byte offset, and a tile row of 16 doubles
-// touched two lines, a 32-column operand row three).  Entries above the diagonal of a
-// diagonal tile and rows >= n of the last tile row are storage only.  LDS factors keep
-// the packed rows (roff).
-__host__ __device__ __forceinline__ int toff(int i, int j) {
-    const int I = i >> 4;
-    return ((I * (I + 1) >> 1) + (j >> 4)) * 256 + ((i & 15) << 4) + (j & 15);
-}
-// doubles of a tiled factor of order n, plus one tile that reads past a row's end may touch
-__host__ __device__ __forceinline__ int tiled_size(int n) {
-    const int T = (n + 15) >> 4;
-    return (T * (T + 1) / 2 + 1) * 256;
-}
-template <class HP>
-struct HAddr {   // offset of entry (i, j <= i) of the factor behind a pointer of type HP
-    static constexpr bool TILED =
-        std::is_same<typename std::remove_cv<typename std::remove_pointer<HP>::type>::type, gdouble>::value;
-    __device__ static __forceinline__ int off(int i, int j) { return TILED ? toff(i, j) : roff(i) + j; }
-    // off(i, j) = off(i, 0) + col(j)
-    __device__ static __forceinline__ int col(int j) { return TILED ? ((j >> 4) << 8) + (j & 15) : j; }
-};
-
 // The reduction / slot area `red` of a plan (doubles): [0, 48) the three partial-sum
 // buffers of block_reduce4, [0, 64) also the factorisation's look-ahead rows (ldbuf; no
 // reduction runs inside the factorisation), then single slots, then the pivots.
@@ -257,9 +232,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.scr = p;
     int u = 0;
     // packed K plus one spare row (row n: target of the predicate-free tile stores)
-    // LDS: packed K plus one spare row (row n: target of the predicate-free tile stores);
-    // workspace: tiled (toff), first in the workspace, so 128-byte aligned
-    if (hG) { f.H = w; w += tiled_size(n); } else { f.H = p + u; u += pad2(roff(n + 1) + 16); }
+    if (hG) { f.H = w; w += pad2(roff(n + 1) + 16); } else { f.H = p + u; u += pad2(roff(n + 1) + 16); }
     const int setup = NWAVE * SCR_PER_WAVE;
     // plan 2 with constraint-row arrays at least as large as the setup scratch (8
     // vehicles at Hp 30): the W~ blocks go to the workspace as well, and the setup
@@ -274,7 +247,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
         f.scr = f.rowE;
         f.uni = 0;
     }
-    f.ws = (w + 15) & ~15;   // workgroup stride: keeps every workgroup's factor 128-byte aligned
+    f.ws = w;
     f.ldAlloc = ld;
     f.mcAlloc = pad2(mc);
     return f;
@@ -1142,7 +1115,7 @@ __device__ __forceinline__ void assemble_tiles(const cParams& P, const LT& L, PD
                 const int row = a_ * Hb + l, col = b_ * Hb + lp;
                 double acc = c[di][dj];
                 if (row == col) acc += 2.0 * u2 * P.R[a_] + d[L.m + row] + d[L.m + N + row] + rho;
-                L.H[HAddr<decltype(L.H)>::off(row, col)] = acc;
+                L.H[roff(row) + col] = acc;
             }
     }
 }
@@ -1227,9 +1200,8 @@ __device__ void assemble(const cParams& P, const LT& L, PD d, double rho) {
     }
     PROF_ACC_FINE0(26);
     const int N = L.N;
-    using HA = HAddr<decltype(L.H)>;
-    toeplitz_t_apply(L, L.yb, [&](int e, double tt) { L.H[HA::off(N, e)] = tt; });
-    if (tid == 0) L.H[HA::off(N, N)] = red[0] + d[L.mc - 1] + rho;
+    toeplitz_t_apply(L, L.yb, [&](int e, double tt) { L.H[roff(N) + e] = tt; });
+    if (tid == 0) L.H[roff(N) + N] = red[0] + d[L.mc - 1] + rho;
     bar();
     PROF_ACC_FINE0(27);
 }
@@ -1309,17 +1281,15 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
                                               int nprev, ldouble* ldbuf) {
     const int lane = threadIdx.x & 63;
     PROF_T0_FINE();
-    using HA = HAddr<HP>;
     double p[RS][CB];
-    int ro[RS];   // row starts (clamped rows); a column j at ro + HA::col(j) (uniform)
-    const int cr0 = HA::col(r0);   // the panel's 8 columns lie in one tile of a tiled factor
+    int ro[RS];
 #pragma unroll
     for (int t = 0; t < RS; ++t) {
         const int i = r0 + lane + 64 * t;
-        ro[t] = HA::off(i < n ? i : n - 1, 0);
+        ro[t] = roff(i < n ? i : n - 1);
 #pragma unroll
         for (int c = 0; c < CB; c += 2) {
-            const double2v v = ld2(H + ro[t] + cr0 + c);
+            const double2v v = ld2(H + ro[t] + r0 + c);
             p[t][c] = v.x;
             p[t][c + 1] = v.y;
         }
@@ -1334,7 +1304,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         for (int t = 0; t < RS; ++t)
 #pragma unroll
             for (int c = 0; c < CB; c += 2) {
-                const double2v v = ld2(H + ro[t] + HA::col(jp + q * CB) + c);
+                const double2v v = ld2(H + ro[t] + jp + q * CB + c);
                 li[t][c] = v.x;
                 li[t][c + 1] = v.y;
             }
@@ -1446,7 +1416,7 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
         if (i < n) {
 #pragma unroll
             for (int c = 0; c < CB; c += 2)
-                if (c < jb && c <= lane + 64 * t) st2(H + ro[t] + cr0 + c, double2v{p[t][c], p[t][c + 1]});
+                if (c < jb && c <= lane + 64 * t) st2(H + ro[t] + r0 + c, double2v{p[t][c], p[t][c + 1]});
         }
     }
     // rows r0 + 8 .. r0 + 15 (the next panel's diagonal-block rows), D-scaled, for the
@@ -1538,34 +1508,22 @@ typedef double double4v __attribute__((ext_vector_type(4)));
 template <int U, int KS, class HP>
 __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1, const ldouble* dcur,
                                                      int wave, int nwave, int part = 0, int np = 1) {
-    using HA = HAddr<HP>;
     const int lane = threadIdx.x & 63, lr = lane & 15, lk = lane >> 4;
     double dk[KS];
 #pragma unroll
     for (int kk = 0; kk < KS; ++kk) dk[kk] = dcur[4 * kk + lk];
-    // the tile grid: on a tiled factor the storage tiles (origin g0 = r1 rounded down to
-    // 16, so that every MFMA tile is one storage tile; the columns g0 .. r1 - 1 of tile
-    // column 0 belong to the lead's current panel and are neither stored nor needed),
-    // else the rows / columns from r1
-    const int g0 = HA::TILED ? (r1 & ~15) : r1;
-    const int T = (n - g0 + 15) >> 4;
+    const int T = (n - r1 + 15) >> 4;
     const int ntile = T * (T + 1) / 2;
     int tb = 0, te = ntile;
     if (part != 0) {
         // part p of np: the tile columns from the (p-1)-th to the p-th cut, the k-th cut
-        // being the first tile-column boundary with >= k ntile / np tiles before it.
-        // Tile column 0 is always in part 1; on the shifted grid tile column 1 holds the
-        // group's third and fourth panels, which the lead factors from the group's third
-        // step on, so it is always in part 1 or 2
+        // being the first tile-column boundary with >= k ntile / np tiles before it
+        // (tile column 0 always in part 1)
         int js = 1, cum = T;   // tiles in the tile columns < js
         for (int k = 1; k < np; ++k) {
             while (js < T && np * cum < k * ntile) {
                 cum += T - js;
                 ++js;
-            }
-            if (HA::TILED && g0 < r1 && k == 2 && js < 2 && T > 1) {
-                cum += T - js;
-                js = 2;
             }
             if (k == part - 1) tb = cum;
             if (k == part) te = cum;
@@ -1584,24 +1542,20 @@ __device__ __forceinline__ void trailing_update_mfma(HP H, int n, int j0, int r1
             tri_decode(ntile - 1 - (live ? tu : t), J, I);
             I = T - 1 - I;
             J = T - 1 - J;
-            const int i0 = g0 + 16 * I, k0 = g0 + 16 * J;
+            const int i0 = r1 + 16 * I, k0 = r1 + 16 * J;
             const int ia = min(i0 + lr, n - 1), kb = min(k0 + lr, n - 1);
-            // operand rows ia / kb at the previous panels' columns j0 + 4 kk + lk (j0 a
-            // multiple of 32: on a tiled factor columns j0 .. j0 + 31 are two whole tiles)
-            const int oa = HA::off(ia, 0), ob = HA::off(kb, 0);
+            const int oa = roff(ia) + j0, ob = roff(kb) + j0;
 #pragma unroll
             for (int kk = 0; kk < KS; ++kk) {
-                const int cj = HA::TILED ? HA::col(j0) + ((kk >> 2) << 8) + 4 * (kk & 3) + lk
-                                         : j0 + 4 * kk + lk;
-                a[u][kk] = -H[oa + cj] * dk[kk];
-                b[u][kk] = H[ob + cj];
+                a[u][kk] = -H[oa + 4 * kk + lk] * dk[kk];
+                b[u][kk] = H[ob + 4 * kk + lk];
             }
             const int kc = k0 + lr;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int ci = i0 + lk + 4 * r;
-                ok[u][r] = live && ci < n && kc <= ci && kc >= r1;
-                oc[u][r] = ok[u][r] ? HA::off(ci, kc) : 0;
+                ok[u][r] = live && ci < n && kc <= ci;
+                oc[u][r] = roff(ok[u][r] ? ci : 0) + (ok[u][r] ? kc : 0);
                 acc[u][r] = ok[u][r] ? (double)H[oc[u][r]] : 0.0;
             }
         }
@@ -1733,7 +1687,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n
         for (int t = 0; t < R; ++t) {
             ii[t] = lane + 64 * t;
             ic[t] = ii[t] < n ? ii[t] : n - 1;
-            ro[t] = HAddr<HP>::off(ic[t], 0);   // row start; columns at HAddr::col
+            ro[t] = roff(ic[t]);
             r[t] = ii[t] < n ? bvec[ii[t]] : 0.0;
             xf[t] = 0.0;
         }
@@ -1743,7 +1697,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n
         for (int t = 0; t < R; ++t)
 #pragma unroll
             for (int q = 0; q < SCH; q += 2) {
-                const double2v v = ld2(H + ro[t] + HAddr<HP>::col(jc) + q);   // jc: a chunk in one tile
+                const double2v v = ld2(H + ro[t] + jc + q);
                 dst[t][q] = v.x;
                 dst[t][q + 1] = v.y;
             }
@@ -1753,7 +1707,7 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n
         for (int q = 0; q < SCH; ++q) {
             const int row = jc + q < n ? jc + q : n - 1;
 #pragma unroll
-            for (int t = 0; t < R; ++t) dst[t][q] = H[HAddr<HP>::off(row, ic[t])];
+            for (int t = 0; t < R; ++t) dst[t][q] = H[roff(row) + ic[t]];
         }
     }
     __device__ __forceinline__ void shift() {
@@ -2341,8 +2295,8 @@ PHASE int ph_assemble_factor(Ctx c, double rho) {
 PHASE void ph_init_assemble_factor(Ctx c) {
     LAYDEF;
     assemble(P, L, L.dd, 0.0);
-    const int N = L.N;
-    for (int e = threadIdx.x; e <= N; e += NT) L.H[HAddr<decltype(L.H)>::off(N, e)] = e == N ? 1.0 : 0.0;
+    const int N = L.N, o = roff(N);
+    for (int e = threadIdx.x; e <= N; e += NT) L.H[o + e] = e == N ? 1.0 : 0.0;
     bar();
     cholesky(L);   // P + G'G is positive definite (box and omega rows)
 }
