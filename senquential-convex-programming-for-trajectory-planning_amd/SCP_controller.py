@@ -36,7 +36,6 @@ import functools
 import time
 
 import numpy as np
-import torch
 
 from Config import Config
 from MPC_Iter import MPCclass
@@ -255,18 +254,17 @@ class SCPcontroller:
             u_approx[0] = np.spacing(1)
         res = self.solver.solve(u_warm=np.asarray(u_approx, float).reshape(1, -1), trace=True,
                                 **self._inputs())
-        # the trace goes to pinned host memory asynchronously, queued before the copies
-        # below (same stream), which therefore return with it complete: the log costs one
-        # queued copy inside optimizerTime, and its decode runs only when the log is read
-        tr_host = torch.empty(res.trace.shape[1:], dtype=res.trace.dtype, pin_memory=True)
-        tr_host.copy_(res.trace[0], non_blocking=True)
         u = res.u[0, :self.nVeh * self.Hp].cpu().numpy().reshape(-1, 1)
         status = int(res.status[0].item())
         n_scp = int(res.n_scp[0].item())
+        # only the n_scp trace rows this solve wrote come to the host (the whole
+        # trace_iters-row record, ~600 KB at 8 vehicles and Hp 30, went to a fresh pinned
+        # buffer every solve); the decode runs only when the log is read
+        tr_host = res.trace[0, :n_scp].cpu().numpy()
         m = self.mpc
         # the decode's inputs, host arrays only (the trace rows of this solve and the
         # linearisation): the log keeps neither the controller nor device tensors alive
-        dec = functools.partial(_iteration_log, tr_host.numpy()[:n_scp], n_scp,
+        dec = functools.partial(_iteration_log, tr_host, n_scp,
                                 self.nVeh, self.nObst, self.Hp, self.solver.hp_max,
                                 self.scenario_uLim, m.Mathcal_B.copy(), m.const_term.copy(),
                                 m.Phi_0.copy(), m.Psi_0.copy(), float(np.sum(m.gamma_0)))
