@@ -1375,28 +1375,43 @@ __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0,
     double inv[CB], dg[CB];
     int bad = 0;
     double u0[CB];   // slot 0's unscaled entries (the next step's look-ahead rows)
-    // Column by column, every row at once (round 5): column c's unscaled entries
-    // U[c2][c] = L[c2][c] D_c of the block's rows c2 >= c (lanes c2 of slot 0, D_c on the
-    // diagonal) are broadcast with v_readlane, then every row scales its entry by 1/D_c
-    // and updates its columns > c.  The block's own rows run the same operations, so the
-    // 8 x 8 factorisation on uniform values (152 FP64 operations in every lane, round 3)
-    // and the substitution after it become one sweep of 40 + 36 RS operations; the chain
-    // per column is one readlane link, the reciprocal and two FMAs.
+    // Two columns per round (round 6).  Column c's entries U0 (rows c..7) and column
+    // c + 1's, not yet updated by column c (V, rows c + 1..7), are broadcast with one round
+    // of v_readlane; the pair's pivots come from the 2 x 2 block [d0 b; b e]: d1 = det / d0
+    // with det = d0 e - b^2, so 1/d0 and 1/det are computed side by side and 1/d1 = d0 / det,
+    // instead of 1/d1 after 1/d0 and a second readlane round (the round-5 column-by-column
+    // chain).  Column c + 1 of the block rows, updated by column c (W), is formed on
+    // uniform values with the column-by-column form's own operations, so every entry but
+    // the second pivot of a pair is computed as before.
 #pragma unroll
-    for (int c = 0; c < CB; ++c) {
-        double U[CB];
+    for (int c = 0; c < CB; c += 2) {
+        double U0[CB], V[CB], W[CB];
 #pragma unroll
-        for (int c2 = c; c2 < CB; ++c2) U[c2] = readlane_d(p[0][c], c2);
-        dg[c] = U[c];
-        bad |= !(U[c] > 0.0) || !isfinite(U[c]);
-        inv[c] = recip(U[c]);
+        for (int c2 = c; c2 < CB; ++c2) U0[c2] = readlane_d(p[0][c], c2);
+#pragma unroll
+        for (int c2 = c + 1; c2 < CB; ++c2) V[c2] = readlane_d(p[0][c + 1], c2);
+        const double d0 = U0[c], b = U0[c + 1], e = V[c + 1];
+        const double det = fma(d0, e, -(b * b));
+        const double i0 = recip(d0), rdet = recip(det);
+        const double i1 = d0 * rdet;
+        dg[c] = d0;
+        dg[c + 1] = det * i0;
+        bad |= !(d0 > 0.0) || !isfinite(d0) || !(det > 0.0) || !isfinite(det);
+        inv[c] = i0;
+        inv[c + 1] = i1;
+#pragma unroll
+        for (int c2 = c + 2; c2 < CB; ++c2) W[c2] = fma(-(U0[c2] * i0), b, V[c2]);
         u0[c] = p[0][c];
 #pragma unroll
         for (int t = 0; t < RS; ++t) {
-            const double lc = p[t][c] * inv[c];
+            const double l0 = p[t][c] * i0;
+            const double pc1 = fma(-l0, b, p[t][c + 1]);
+            if (t == 0) u0[c + 1] = pc1;
+            const double l1 = pc1 * i1;
 #pragma unroll
-            for (int c2 = c + 1; c2 < CB; ++c2) p[t][c2] = fma(-lc, U[c2], p[t][c2]);
-            p[t][c] = lc;
+            for (int c2 = c + 2; c2 < CB; ++c2) p[t][c2] = fma(-l1, W[c2], fma(-l0, U0[c2], p[t][c2]));
+            p[t][c] = l0;
+            p[t][c + 1] = l1;
         }
     }
     if (lane < CB && lane < jb) {
