@@ -1744,26 +1744,10 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n
             const int jend = min(n, 64 * (T + 1));
             auto chunk = [&](int jc) {
                 if (jc + SCH < n) load_cols(nxt, jc + SCH);
-                // two rows per readlane round (round 6): r_j and r_j+1 are broadcast
-                // together and x_j+1 = r_j+1 - L[j+1][j] x_j is formed on uniform values
-                // (L[j+1][j] read from its owner lane off the chain), so the chain per two
-                // rows is one readlane link and two FMAs instead of two links
 #pragma unroll
-                for (int q = 0; q < SCH; q += 2) {
+                for (int q = 0; q < SCH; ++q) {
                     const int j = jc + q;
-                    if (j + 1 < jend) {
-                        const double l10 = readlane_d(cur[T][q], (j + 1) & 63);
-                        const double xa = readlane_d(r[T], j & 63), rb = readlane_d(r[T], (j + 1) & 63);
-                        const double xb = rb - l10 * xa;
-                        r[T] -= cur[T][q] * xa;
-                        r[T] -= cur[T][q + 1] * xb;
-                        xf[T] = capture(xb, j + 1, capture(xa, j, xf[T]));
-#pragma unroll
-                        for (int t = T + 1; t < R; ++t) {
-                            r[t] -= cur[t][q] * xa;
-                            r[t] -= cur[t][q + 1] * xb;
-                        }
-                    } else if (j < jend) {
+                    if (j < jend) {
                         const double xj = readlane_d(r[T], j & 63);
                         r[T] -= cur[T][q] * xj;
                         xf[T] = capture(xj, j, xf[T]);
@@ -1791,29 +1775,16 @@ struct Solver {   // SCH: chunk (columns / rows) streamed per step group; RTN: n
             const int jstart = (T == R - 1) ? jlast : 64 * T + 64 - SCH;
             auto chunk = [&](int jc) {
                 if (jc > 0) load_rows(nxt, jc - SCH);
-                // two rows per readlane round, as forward: x_j-1 = r_j-1 - L[j][j-1] x_j
 #pragma unroll
-                for (int q = SCH - 1; q >= 0; q -= 2) {
+                for (int q = SCH - 1; q >= 0; --q) {
                     const int j = jc + q;
                     if (j < n) {
-                        const double l10 = readlane_d(cur[T][q], (j - 1) & 63);
-                        const double xa = readlane_d(r[T], j & 63), rb = readlane_d(r[T], (j - 1) & 63);
-                        const double xb = rb - l10 * xa;
+                        const double xj = readlane_d(r[T], j & 63);
                         // the owner slot first: it carries the next step's broadcast
-                        r[T] -= cur[T][q] * xa;
-                        r[T] -= cur[T][q - 1] * xb;
-                        xf[T] = capture(xb, j - 1, capture(xa, j, xf[T]));
+                        r[T] -= cur[T][q] * xj;
+                        xf[T] = capture(xj, j, xf[T]);
 #pragma unroll
-                        for (int t = 0; t < T; ++t) {
-                            r[t] -= cur[t][q] * xa;
-                            r[t] -= cur[t][q - 1] * xb;
-                        }
-                    } else if (j - 1 < n) {
-                        const double xj = readlane_d(r[T], (j - 1) & 63);
-                        r[T] -= cur[T][q - 1] * xj;
-                        xf[T] = capture(xj, j - 1, xf[T]);
-#pragma unroll
-                        for (int t = 0; t < T; ++t) r[t] -= cur[t][q - 1] * xj;
+                        for (int t = 0; t < T; ++t) r[t] -= cur[t][q] * xj;
                     }
                 }
                 shift();
