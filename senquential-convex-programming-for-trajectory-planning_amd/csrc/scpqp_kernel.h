@@ -183,17 +183,11 @@ __host__ __device__ constexpr int red_size(bool hG) { return kPivSlot + 2 * (hG 
 // the lean plan 1 (W~ blocks and constraint rows in the workspace beside the vectors) at
 // two workgroups per CU (c5, Hp 30), or four (the round-6 c2 residency experiment)
 __host__ __device__ constexpr bool lean_plan(bool hG, bool vG, int occ) { return !hG && vG && (occ == 2 || occ == 4); }
-// Plan 1 at three workgroups per CU (c2, c4) keeps one of the nine constraint vectors in
-// LDS: tv, the operand of every G' t (gt_apply_fin), written row by row and read by the
-// incident-row sums of other threads, so that each G' t product and the barrier before it
-// wait on LDS instead of an L2 round trip (round 6; 2.3 KB of the 2.9 KB left at three per CU)
-__host__ __device__ constexpr bool tv_lds(bool hG, bool vG, bool lean) { return vG && !hG && !lean; }
 
 struct Off {
     int x0, u0, ec, g, p0, ref, ob, ub, pb, ya, yb, qs, rowE, rowW, rowH, rinfo;
     int z, dz, rhs, rd, dinv, red, scr;
     int H, Wt, vec;     // H and vec in LDS (after persist) or workspace, see hG / vG
-    int tv;             // the G't operand vector in LDS on plan 1 at three per CU (tv_lds)
     int persist, uni, ws;
     int ldAlloc, mcAlloc;
 };
@@ -234,9 +228,6 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     f.rd = p; p += pad2(n);
     f.dinv = p; p += pad2(n);
     f.red = p; p += red_size(hG);   // kRedFlag ... kPivSlot
-    const bool tvL = tv_lds(hG, vG, lean);
-    f.tv = tvL ? p : -1;
-    if (tvL) p += pad2(mc);
     f.persist = p;
     f.scr = p;
     int u = 0;
@@ -250,7 +241,7 @@ __host__ __device__ inline Off plan_offsets(int V, int O, int Hm, bool hG, bool 
     const bool wG = (hG && vG && (n + 63) / 64 == 4) || lean;   // = Lay::WGLOBAL
     const bool rows_scr = wG && !lean && f.rinfo + pad2((m + 1) / 2) - f.rowE >= setup;
     if (wG) { f.Wt = w; w += pad2(4 * Hm * nb); } else { f.Wt = p + u; u += pad2(4 * Hm * nb); }
-    if (vG) { f.vec = w; w += (tvL ? 8 : 9) * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
+    if (vG) { f.vec = w; w += 9 * pad2(mc); } else { f.vec = p + u; u += 9 * pad2(mc); }
     f.uni = u > setup ? u : setup;
     if (rows_scr) {
         f.scr = f.rowE;
@@ -284,10 +275,7 @@ struct Lay {
     RIT* rinfo;
     WT* Wt;
     HT* H;
-    static constexpr bool TVL = tv_lds(HG, VG, LEAN);
-    using TT = typename std::conditional<TVL, ldouble, VT>::type;
-    VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la;
-    TT* tv;
+    VT *s, *lam, *ds, *dl, *rp, *dd, *sa, *la, *tv;
 };
 
 // Problem shapes compiled as constants (template SH): the vehicle count, obstacle
@@ -352,8 +340,7 @@ __device__ __forceinline__ Lay<HG, VG, RM, OCC> make_lay(ldouble* lds, gdouble* 
     if constexpr (VG) vb = ws + f.vec; else vb = lds + f.vec;
     const int st = f.mcAlloc;
     L.s = vb; L.lam = vb + st; L.ds = vb + 2 * st; L.dl = vb + 3 * st; L.rp = vb + 4 * st;
-    L.dd = vb + 5 * st; L.sa = vb + 6 * st; L.la = vb + 7 * st;
-    if constexpr (Lay<HG, VG, RM, OCC>::TVL) L.tv = lds + f.tv; else L.tv = vb + 8 * st;
+    L.dd = vb + 5 * st; L.sa = vb + 6 * st; L.la = vb + 7 * st; L.tv = vb + 8 * st;
     return L;
 }
 
