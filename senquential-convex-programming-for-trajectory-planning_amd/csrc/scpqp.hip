@@ -103,6 +103,7 @@ struct scpqp_handle {
 namespace {
 
 const size_t kLdsLimit = 163840;
+const size_t kLdsGranule = 2048;
 // workgroups per CU at three waves per SIMD (the 168-VGPR budget of OCC = 3)
 const int kMaxPerCU = 12 / NWAVE;
 
@@ -131,7 +132,10 @@ int plan(scpqp_handle* h) {
             const Off f = plan_offsets(V, O, Hm, cfg >= 2, cfg >= 1, lean);
             const size_t lds = (size_t)(f.persist + f.uni) * sizeof(double);
             if (lds > kLdsLimit) continue;
-            int perCU = (int)(kLdsLimit / lds);
+            // residency at the LDS allocation granularity: a c2 plan of 53,888 B (3 x 161,664 B
+            // by byte count) ran as if fewer than three workgroups fit per CU (round 6,
+            // profiles/r06_ab_tv_lds.txt); 2 KB granules agree with every plan measured
+            int perCU = (int)(kLdsLimit / ((lds + kLdsGranule - 1) / kLdsGranule * kLdsGranule));
             // beyond 3 waves per SIMD the register budget, not LDS, bounds residency
             if (perCU > kMaxPerCU) perCU = kMaxPerCU;
             if (cfg == 1 && !lean && perCU < 3) continue;   // OCC 2 runs plan 1 lean
