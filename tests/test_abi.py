@@ -120,3 +120,42 @@ def test_ctypes_layout_matches_header(tmp_path):
         assert int(got[cn]) == C.sizeof(cls), cn
         for f, _ in cls._fields_:
             assert int(got[f"{cn}.{f}"]) == getattr(cls, f).offset, f"{cn}.{f}"
+
+
+def test_every_kernel_instantiation_in_exactly_one_group():
+    """The host side (scpqp.hip) declares every kernel instantiation extern
+    (SCPQP_KERNEL_LIST); kernels.hip must define each in exactly one of its groups, or the
+    library fails to link (missing) or compiles a kernel twice (duplicate)."""
+    import re
+    csrc = os.path.join(ROOT, "senquential-convex-programming-for-trajectory-planning_amd", "csrc")
+    host = open(os.path.join(csrc, "scpqp.hip")).read()
+    kern = open(os.path.join(csrc, "kernels.hip")).read()
+    body = host[host.index("#define SCPQP_RT_LIST"):host.index("#define SCPQP_EXTERN_LAUNCH")]
+    listed = set()
+    for hgv, vgv in re.findall(r"SCPQP_RT_LIST\(X, (true|false), (true|false)\)", body):
+        for r, o in ((1, 2), (1, 3), (2, 2), (2, 3), (3, 2), (3, 3), (4, 2), (4, 3)):
+            listed.add((hgv, vgv, str(r), str(o), "0"))
+    for t in re.findall(r"X\((\w+), (\w+), (\d), (\d), (\d)\)", body.split("#define SCPQP_KERNEL_LIST")[1]):
+        listed.add(t)
+    inst = re.findall(r"SCPQP_INST\((\w+), (\w+), (\d), (\d), (\d)\)", kern.split("#define SCPQP_INST")[1])
+    diag = set(re.findall(r"#ifdef SCPQP_DIAG[^\n]*\nSCPQP_INST\((\w+), (\w+), (\d), (\d), (\d)\)", kern))
+    prod = [t for t in inst if t not in diag]
+    assert len(prod) == len(set(prod)), "an instantiation appears in two groups"
+    assert set(prod) == listed
+
+
+def test_c2_kernel_register_budget_from_code_object():
+    """The c2 / c4 kernel's descriptor (tools/kernel_resources.py, no GPU needed): compiled for
+    three workgroups per CU (<= 168 VGPRs) with its stack at <= 260 B per lane (verdict r05
+    item 3), and no static LDS beside the plan's dynamic LDS."""
+    import sys as _sys
+    _sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import kernel_resources as KR
+    ks = [k for k in KR.kernels(LB.LIB_PATH)]
+    names = KR.demangle([k["name"] for k in ks])
+    c2 = [k for k, d in zip(ks, names) if "scp_kernel<false, true, 2, 3, 1>" in d]
+    assert len(c2) == 1
+    k = c2[0]
+    assert k["vgpr_count"] + k.get("agpr_count", 0) <= 168
+    assert k["private_segment_fixed_size"] <= 260
+    assert k["group_segment_fixed_size"] == 0
