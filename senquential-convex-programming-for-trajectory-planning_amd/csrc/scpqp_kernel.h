@@ -1275,11 +1275,18 @@ __device__ __forceinline__ void lead_prio_down() { __builtin_amdgcn_s_setprio(0)
 //  * every row then applies the block's factor by forward substitution
 //    (p_ic -= (p_ic' / D_c') U_cc', U = L D unscaled), which for the block's own rows
 //    repeats the uniform factorisation operation for operation.
-template <int RS, class HP>
+template <int RS, bool OPQ, class HP>
 __device__ __forceinline__ void panel_factor(HP H, ldouble* dinv, int n, int r0, int jb, int jp,
                                               const ldouble* dprev, ldouble* dout, lint* flag,
                                               int nprev, ldouble* ldbuf) {
-    const int lane = threadIdx.x & 63;
+    // OPQ (kernels with more than two row slots, c3): the lane index through an empty
+    // volatile asm, so that the values derived from it (the identity padding, the look-ahead
+    // row addresses) are formed per panel step instead of being hoisted out of the step loop,
+    // where at RMAX = 4 they were spilled to scratch and reloaded on the lead's chain every
+    // step (c3 +4.5 %; at RMAX = 2 nothing is spilled and the recomputation costs c2 3 %:
+    // profiles/r06_ab_panel_lane.txt)
+    int lane = threadIdx.x & 63;
+    if constexpr (OPQ) asm volatile("" : "+v"(lane));
     PROF_T0_FINE();
     double p[RS][CB];
     int ro[RS];
@@ -1625,8 +1632,9 @@ __device__ bool cholesky(const LT& L) {
             // runs with one register row (half the VALU work of the chain)
             ldouble* dn = dbuf + (s % (2 * G)) * CB;
             lead_prio_up();
-            if (RS == 1 || n - r0 <= 64) panel_factor<1>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
-            else panel_factor<RS>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
+            constexpr bool OPQ = RS > 2;
+            if (RS == 1 || n - r0 <= 64) panel_factor<1, OPQ>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
+            else panel_factor<RS, OPQ>(L.H, L.dinv, n, r0, jb, jp, dprev, dn, flag + par, np, ldbuf);
             lead_prio_down();
         } else if (jp >= 0 || (G > 1 && s >= G)) {
             const int tw = (wave_id() - L.lead + NWAVE - 1) % NWAVE;   // 0 .. NWAVE-2
